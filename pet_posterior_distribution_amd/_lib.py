@@ -1,0 +1,110 @@
+"""ctypes binding of libpetdiff.so (the C ABI declared in include/petdiff.h).
+
+The shared library is built in-tree by ``__graft_entry__.build()`` (or
+``make -C pet_posterior_distribution_amd/csrc``).  There is no fallback: if the
+library is missing every entry point raises ``RuntimeError`` -- the product path
+never silently computes on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libpetdiff.so')
+
+PETDIFF_OK, PETDIFF_ERR_INVALID, PETDIFF_ERR_HIP, PETDIFF_ERR_UNSUPPORTED = 0, 1, 2, 3
+DTYPE_F32, DTYPE_BF16 = 0, 1
+LEARN_FIXED, LEARN, LEARN_RANGED = 0, 1, 2
+PARAM_EPS, PARAM_X0, PARAM_V, PARAM_XPREV = 0, 1, 2, 3
+NTAB = 13
+NUM_LAYERS = 10
+LAYER_NAMES = ['down0', 'down1', 'down2', 'down3', 'up0.conv2', 'up0.block', 'up1.conv2',
+               'up1.block', 'up2.conv2', 'up2.block+final+p_sample']
+
+
+class PetdiffConfig(C.Structure):
+    _fields_ = [('n_roi', C.c_int), ('n_par', C.c_int), ('n_frames', C.c_int), ('n_cond_rows', C.c_int),
+                ('num_filt_start', C.c_int), ('depth', C.c_int), ('kernel_size', C.c_int),
+                ('pool_size', C.c_int), ('sin_emb_dim', C.c_int), ('enc_size', C.c_int * 3),
+                ('latent_dim', C.c_int), ('timesteps', C.c_int), ('learn_variance', C.c_int),
+                ('parameterization', C.c_int), ('dtype', C.c_int)]
+
+
+# (name, restype, argtypes) of every exported symbol in include/petdiff.h
+SYMBOLS = [
+    ('petdiff_default_config', C.c_int, [C.POINTER(PetdiffConfig)]),
+    ('petdiff_param_count', C.c_size_t, [C.POINTER(PetdiffConfig)]),
+    ('petdiff_create', C.c_int, [C.POINTER(PetdiffConfig), C.c_void_p, C.c_size_t, C.c_int, C.POINTER(C.c_void_p)]),
+    ('petdiff_destroy', C.c_int, [C.c_void_p]),
+    ('petdiff_set_schedule', C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    ('petdiff_cosine_schedule', C.c_int, [C.c_int, C.c_double, C.c_double, C.c_void_p]),
+    ('petdiff_set_conditions', C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
+    ('petdiff_forward', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                  C.c_void_p]),
+    ('petdiff_p_sample', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                   C.c_uint64, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                   C.c_void_p]),
+    ('petdiff_generate', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
+                                   C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                   C.c_void_p]),
+    ('petdiff_posterior_stats', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
+                                          C.c_void_p]),
+    ('petdiff_set_timing', C.c_int, [C.c_void_p, C.c_int]),
+    ('petdiff_get_timing', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    ('petdiff_last_error', C.c_char_p, []),
+    # Metropolis-Hastings / SRTM2 (include/petmh.h)
+    ('petmh_srtm2_tac', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                  C.c_void_p, C.c_void_p, C.c_void_p]),
+    ('petmh_create', C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
+    ('petmh_destroy', C.c_int, [C.c_void_p]),
+    ('petmh_run', C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_p,
+                            C.c_void_p, C.c_void_p]),
+    ('petmh_logp', C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
+]
+
+_lib = None
+
+
+class PetdiffError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libpetdiff.so once; raise loudly if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f'libpetdiff.so not found at {LIB_PATH}: build it with '
+                           f'`python -c "import __graft_entry__ as g; g.build()"` (no CPU fallback exists)')
+    L = C.CDLL(LIB_PATH)
+    for name, res, args in SYMBOLS:
+        fn = getattr(L, name, None)
+        if fn is None:
+            continue
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def last_error():
+    return lib().petdiff_last_error().decode(errors='replace')
+
+
+def check(rc, what=''):
+    """Raise the reference's exception type for a C-ABI status code."""
+    if rc == PETDIFF_OK:
+        return
+    msg = f'{what}: {last_error()}' if what else last_error()
+    if rc == PETDIFF_ERR_INVALID:
+        raise ValueError(msg)
+    if rc == PETDIFF_ERR_UNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise PetdiffError(msg)
+
+
+def exported_symbols():
+    """Names of the C entry points this binding expects (for the load test)."""
+    return [s[0] for s in SYMBOLS]

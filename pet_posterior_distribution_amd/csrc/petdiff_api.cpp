@@ -1,0 +1,735 @@
+// C-ABI implementation of libpetdiff.so (declared in include/petdiff.h).
+//
+// Host-side runtime of the sampler: weight packing into the MFMA layouts,
+// per-level condition/time map folding, workspace management, the reverse
+// loop (eager or captured once into a hipGraph and replayed), posterior
+// statistics and per-layer event timing.
+#include "petdiff.h"
+#include "petdiff_internal.h"
+
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+using namespace petdiff;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPC(expr)                                                                        \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return fail(PETDIFF_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));    \
+  } while (0)
+
+#define CHK(expr)                   \
+  do {                              \
+    int r_ = (expr);                \
+    if (r_ != PETDIFF_OK) return r_; \
+  } while (0)
+
+uint16_t f2bf(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+struct Spec {
+  std::string name;
+  std::vector<int> shape;
+  size_t off;
+  size_t size;
+};
+
+// Ordered tensor list of the weight blob (see petdiff.h); mirrors networks.py:781-992.
+std::vector<Spec> make_spec(const petdiff_config& c, int n_out) {
+  std::vector<Spec> s;
+  size_t off = 0;
+  auto add = [&](const std::string& n, std::vector<int> sh) {
+    size_t sz = 1;
+    for (int d : sh) sz *= (size_t)d;
+    s.push_back({n, sh, off, sz});
+    off += sz;
+  };
+  std::vector<int> dl{c.n_roi};
+  for (int d = 1; d < c.depth; ++d) dl.push_back((dl.back() + 1) / c.pool_size);
+  add("time_mlp.kernel", {c.sin_emb_dim, c.n_roi});
+  add("time_mlp.bias", {c.n_roi});
+  int prev = c.n_frames;
+  for (int i = 0; i < 3; ++i) {
+    add("cond_enc.hidden" + std::to_string(i) + ".kernel", {prev, c.enc_size[i]});
+    add("cond_enc.hidden" + std::to_string(i) + ".bias", {c.enc_size[i]});
+    prev = c.enc_size[i];
+  }
+  add("cond_enc.z.kernel", {prev, c.latent_dim});
+  add("cond_enc.z.bias", {c.latent_dim});
+  int cin = c.n_par;
+  for (int d = 0; d < c.depth; ++d) {
+    const int L = dl[d], cout = c.num_filt_start << d, ci = c.n_cond_rows + 1 + cin;
+    const std::string p = "down" + std::to_string(d);
+    add(p + ".time_proj.kernel", {c.n_roi, L});
+    add(p + ".time_proj.bias", {L});
+    add(p + ".label_proj.kernel", {c.latent_dim, L});
+    add(p + ".label_proj.bias", {L});
+    add(p + ".conv.kernel", {c.kernel_size, ci, cout});
+    add(p + ".conv.bias", {cout});
+    add(p + ".res.kernel", {1, ci, cout});
+    add(p + ".res.bias", {cout});
+    cin = cout;
+  }
+  for (int u = 0; u < c.depth - 1; ++u) {
+    const int L = dl[c.depth - 1 - u], cout = c.num_filt_start << (c.depth - 2 - u);
+    const int ci = c.n_cond_rows + 1 + cin;
+    const std::string p = "up" + std::to_string(u);
+    add(p + ".time_proj.kernel", {c.n_roi, L});
+    add(p + ".time_proj.bias", {L});
+    add(p + ".label_proj.kernel", {c.latent_dim, L});
+    add(p + ".label_proj.bias", {L});
+    add(p + ".upconv.kernel", {c.pool_size, ci, cout});
+    add(p + ".upconv.bias", {cout});
+    add(p + ".conv.kernel", {c.kernel_size, 2 * cout, cout});
+    add(p + ".conv.bias", {cout});
+    add(p + ".res.kernel", {1, 2 * cout, cout});
+    add(p + ".res.bias", {cout});
+    cin = cout;
+  }
+  add("final.kernel", {1, c.num_filt_start, n_out});
+  add("final.bias", {n_out});
+  return s;
+}
+
+bool is_shipped_arch(const petdiff_config& c) {
+  return c.n_roi == 48 && c.n_par == 2 && c.n_frames == 54 && c.n_cond_rows == 49 && c.num_filt_start == 128 &&
+         c.depth == 4 && c.kernel_size == 6 && c.pool_size == 2 && c.sin_emb_dim == 64 && c.enc_size[0] == 256 &&
+         c.enc_size[1] == 128 && c.enc_size[2] == 64 && c.latent_dim == 32;
+}
+
+// geometry of the 7 condition-carrying levels (4 down blocks + 3 up-sampling convs)
+struct CondLevel {
+  const char* prefix;     // "down0" ...
+  const char* conv;       // "conv" or "upconv"
+  bool res;               // has a residual conv folded in
+  int Lseq;               // length of the label/time sequence
+  int Lout;               // output length of the conv
+  int taps, padl, ups;
+  int cin_full, cout;
+};
+
+const CondLevel kLevels[7] = {
+    {"down0", "conv", true, 48, 48, 6, 2, 0, 52, 128},
+    {"down1", "conv", true, 24, 24, 6, 2, 0, 178, 256},
+    {"down2", "conv", true, 12, 12, 6, 2, 0, 306, 512},
+    {"down3", "conv", true, 6, 6, 6, 2, 0, 562, 1024},
+    {"up0", "upconv", false, 6, 12, 2, 0, 1, 1074, 512},
+    {"up1", "upconv", false, 12, 24, 2, 0, 1, 562, 256},
+    {"up2", "upconv", false, 24, 48, 2, 0, 1, 306, 128},
+};
+
+struct ConvLayer {
+  int kind;
+  const char* wname;       // weight prefix of the conv ("down1.conv", "up0.upconv", ...)
+  const char* resname;     // residual kernel or nullptr
+  int taps, padl;
+  int cin_full, xoff, cin_x, cout;
+  int cond_level;          // index into kLevels or -1 (bias only)
+};
+
+const ConvLayer kConv[kNumConvLayers] = {
+    {LK_DOWN1, "down1.conv", "down1.res", 6, 2, 178, 50, 128, 256, 1},
+    {LK_DOWN2, "down2.conv", "down2.res", 6, 2, 306, 50, 256, 512, 2},
+    {LK_DOWN3, "down3.conv", "down3.res", 6, 2, 562, 50, 512, 1024, 3},
+    {LK_UP0_CONV2, "up0.upconv", nullptr, 2, 0, 1074, 50, 1024, 512, 4},
+    {LK_UP0_BLOCK, "up0.conv", "up0.res", 6, 2, 1024, 0, 1024, 512, -1},
+    {LK_UP1_CONV2, "up1.upconv", nullptr, 2, 0, 562, 50, 512, 256, 5},
+    {LK_UP1_BLOCK, "up1.conv", "up1.res", 6, 2, 512, 0, 512, 256, -1},
+    {LK_UP2_CONV2, "up2.upconv", nullptr, 2, 0, 306, 50, 256, 128, 6},
+    {LK_UP2_BLOCK, "up2.conv", "up2.res", 6, 2, 256, 0, 256, 128, -1},
+};
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~DevBuf() { if (p) (void)hipFree(p); }
+  hipError_t alloc(size_t b) {
+    if (b <= bytes && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    hipError_t e = hipMalloc(&p, b ? b : 16);
+    if (e == hipSuccess) bytes = b;
+    return e;
+  }
+  template <typename T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct GraphEntry {
+  hipGraphExec_t exec = nullptr;
+  hipGraph_t graph = nullptr;
+};
+
+}  // namespace
+
+struct petdiff_ctx {
+  petdiff_config cfg;
+  int device = 0;
+  int n_out = 4;
+  std::vector<Spec> spec;
+  std::map<std::string, size_t> off;
+  DevBuf w32;                        // fp32 Keras blob on device
+  DevBuf wpack[kNumConvLayers];      // packed conv weights (bf16 or f32)
+  DevBuf w0;                         // down0 x weights [6][2][128] fp32 (res folded)
+  DevBuf bias_only[kNumConvLayers];  // conv bias + res bias for up blocks
+  DevBuf tmap[7], cmap[7];           // per cond level
+  DevBuf tab;                        // [kNTab][T]
+  DevBuf temb, tseq;                 // [T][48], scratch [T][L]
+  int T = 0;
+  bool sched_set = false;
+  int n_tac = 0;
+  DevBuf enc_a, enc_b;               // encoder scratch
+  // workspace
+  int B_cap = 0;
+  DevBuf s0, p0, s1, p1, s2, p2, d3, u0, b0, u1, b1, u2;
+  DevBuf xa, xb, tacbuf, tbuf, rng;
+  hipStream_t cap_stream = nullptr;
+  std::map<std::vector<int>, GraphEntry> graphs;
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_used;
+  size_t ev_next = 0;
+
+  const float* W(const std::string& n) const { return w32.as<float>() + off.at(n); }
+  size_t act_bytes() const { return cfg.dtype == PETDIFF_DTYPE_BF16 ? 2 : 4; }
+};
+
+namespace {
+
+template <typename T, typename H>
+int pack_conv(petdiff_ctx* h, const std::vector<float>& wk_host, int li) {
+  const ConvLayer& cl = kConv[li];
+  constexpr int KC = sizeof(T) == 2 ? 32 : 16;
+  constexpr int EPC = KC / 4;
+  const Spec* sk = nullptr;
+  const Spec* sr = nullptr;
+  for (auto& s : h->spec) {
+    if (s.name == std::string(cl.wname) + ".kernel") sk = &s;
+    if (cl.resname && s.name == std::string(cl.resname) + ".kernel") sr = &s;
+  }
+  if (!sk) return fail(PETDIFF_ERR_INVALID, "missing weight " + std::string(cl.wname));
+  const float* wk = wk_host.data() + sk->off;
+  const float* wr = sr ? wk_host.data() + sr->off : nullptr;
+  const int NC = cl.cin_x / KC, nNT = cl.cout / kNT;
+  std::vector<H> out((size_t)nNT * NC * cl.taps * kNT * KC);
+  size_t q = 0;
+  for (int nt = 0; nt < nNT; ++nt)
+    for (int kc = 0; kc < NC; ++kc)
+      for (int j = 0; j < cl.taps; ++j)
+        for (int n = 0; n < kNT; ++n)
+          for (int p = 0; p < 4; ++p) {
+            const int c = p ^ ((n >> 2) & 3);
+            for (int e = 0; e < EPC; ++e) {
+              const int ci = cl.xoff + kc * KC + c * EPC + e;
+              const int co = nt * kNT + n;
+              float v = wk[((size_t)j * cl.cin_full + ci) * cl.cout + co];
+              if (wr && j == cl.padl) v += wr[(size_t)ci * cl.cout + co];
+              if constexpr (sizeof(H) == 2) out[q++] = f2bf(v);
+              else out[q++] = v;
+            }
+          }
+  HIPC(h->wpack[li].alloc(out.size() * sizeof(H)));
+  HIPC(hipMemcpy(h->wpack[li].p, out.data(), out.size() * sizeof(H), hipMemcpyHostToDevice));
+  return PETDIFF_OK;
+}
+
+int ensure_workspace(petdiff_ctx* h, int B) {
+  if (B <= h->B_cap) return PETDIFF_OK;
+  const size_t e = h->act_bytes();
+  const size_t Bz = (size_t)B;
+  HIPC(h->s0.alloc(Bz * 48 * 128 * e));
+  HIPC(h->p0.alloc(Bz * 24 * 128 * e));
+  HIPC(h->s1.alloc(Bz * 24 * 256 * e));
+  HIPC(h->p1.alloc(Bz * 12 * 256 * e));
+  HIPC(h->s2.alloc(Bz * 12 * 512 * e));
+  HIPC(h->p2.alloc(Bz * 6 * 512 * e));
+  HIPC(h->d3.alloc(Bz * 6 * 1024 * e));
+  HIPC(h->u0.alloc(Bz * 12 * 512 * e));
+  HIPC(h->b0.alloc(Bz * 12 * 512 * e));
+  HIPC(h->u1.alloc(Bz * 24 * 256 * e));
+  HIPC(h->b1.alloc(Bz * 24 * 256 * e));
+  HIPC(h->u2.alloc(Bz * 48 * 128 * e));
+  HIPC(h->xa.alloc(Bz * 96 * 4));
+  HIPC(h->xb.alloc(Bz * 96 * 4));
+  HIPC(h->tacbuf.alloc(Bz * 4));
+  HIPC(h->tbuf.alloc(Bz * 4));
+  HIPC(h->rng.alloc(16));
+  // workspace moved: cached graphs hold stale pointers
+  for (auto& kv : h->graphs) {
+    if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+    if (kv.second.graph) (void)hipGraphDestroy(kv.second.graph);
+  }
+  h->graphs.clear();
+  h->B_cap = B;
+  return PETDIFF_OK;
+}
+
+hipEvent_t next_event(petdiff_ctx* h) {
+  if (h->ev_next >= h->ev_pool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    h->ev_pool.push_back(e);
+  }
+  return h->ev_pool[h->ev_next++];
+}
+
+struct StepIO {
+  const float* x_in;
+  int t_uniform;              // >= 0: all samples use this t
+  const int* tvec;            // else per-sample t (device)
+  const int* tac;             // device or null
+  FinalArgs fin;
+};
+
+template <typename T>
+int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
+  // layer 0: down0 on VALU
+  auto timed = [&](int layer, auto&& fn) -> int {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (h->timing) {
+      e0 = next_event(h);
+      e1 = next_event(h);
+      if (e0) (void)hipEventRecord(e0, s);
+    }
+    hipError_t e = fn();
+    if (e != hipSuccess) return fail(PETDIFF_ERR_HIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
+    if (h->timing && e0 && e1) {
+      (void)hipEventRecord(e1, s);
+      h->ev_used.push_back({layer, {e0, e1}});
+    }
+    return PETDIFF_OK;
+  };
+  Down0Args d0{};
+  d0.x = io.x_in;
+  d0.w0 = h->w0.as<float>();
+  d0.cmap = h->cmap[0].as<float>();
+  d0.tmap = h->tmap[0].as<float>();
+  d0.tac = io.tac;
+  d0.tvec = io.tvec;
+  d0.t_uniform = io.t_uniform;
+  d0.s0 = h->s0.p;
+  d0.p0 = h->p0.p;
+  d0.B = B;
+  CHK(timed(0, [&] { return launch_down0<T>(d0, s); }));
+
+  struct LIO { const void* s1; int c1; const void* s2; int c2; void* out; void* pool; };
+  const LIO lio[kNumConvLayers] = {
+      {h->p0.p, 128, nullptr, 0, h->s1.p, h->p1.p},
+      {h->p1.p, 256, nullptr, 0, h->s2.p, h->p2.p},
+      {h->p2.p, 512, nullptr, 0, h->d3.p, nullptr},
+      {h->d3.p, 1024, nullptr, 0, h->u0.p, nullptr},
+      {h->s2.p, 512, h->u0.p, 512, h->b0.p, nullptr},
+      {h->b0.p, 512, nullptr, 0, h->u1.p, nullptr},
+      {h->s1.p, 256, h->u1.p, 256, h->b1.p, nullptr},
+      {h->b1.p, 256, nullptr, 0, h->u2.p, nullptr},
+      {h->s0.p, 128, h->u2.p, 128, nullptr, nullptr},
+  };
+  for (int li = 0; li < kNumConvLayers; ++li) {
+    const ConvLayer& cl = kConv[li];
+    ConvArgs<T> a{};
+    a.src1 = reinterpret_cast<const T*>(lio[li].s1);
+    a.c1 = lio[li].c1;
+    a.src2 = reinterpret_cast<const T*>(lio[li].s2);
+    a.c2 = lio[li].c2;
+    a.wpack = h->wpack[li].as<T>();
+    a.out = reinterpret_cast<T*>(lio[li].out);
+    a.out_pool = reinterpret_cast<T*>(lio[li].pool);
+    if (cl.cond_level >= 0) {
+      a.cmap = h->cmap[cl.cond_level].as<float>();
+      a.tmap = h->tmap[cl.cond_level].as<float>();
+    } else {
+      a.bias = h->bias_only[li].as<float>();
+    }
+    a.tac = io.tac;
+    a.tvec = io.tvec;
+    a.t_uniform = io.t_uniform;
+    a.B = B;
+    a.cout = cl.cout;
+    if (li == kNumConvLayers - 1) a.fin = io.fin;
+    CHK(timed(1 + li, [&] { return launch_conv<T>(cl.kind, a, s); }));
+  }
+  return PETDIFF_OK;
+}
+
+int network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
+  if (!h->sched_set) return fail(PETDIFF_ERR_INVALID, "schedule not set (petdiff_set_schedule)");
+  if (h->n_tac <= 0) return fail(PETDIFF_ERR_INVALID, "conditions not set (petdiff_set_conditions)");
+  if (h->cfg.dtype == PETDIFF_DTYPE_BF16) return run_network<bf16>(h, io, B, s);
+  return run_network<float>(h, io, B, s);
+}
+
+FinalArgs base_final(petdiff_ctx* h) {
+  FinalArgs f{};
+  f.wf = h->W("final.kernel");
+  f.bf = h->W("final.bias");
+  f.n_out = h->n_out;
+  f.tab = h->tab.as<float>();
+  f.T = h->T;
+  f.learn_mode = h->cfg.learn_variance;
+  f.param_mode = h->cfg.parameterization;
+  f.rng = h->rng.as<unsigned long long>();
+  return f;
+}
+
+int valid_handle(petdiff_handle h) {
+  if (!h) return fail(PETDIFF_ERR_INVALID, "null handle");
+  HIPC(hipSetDevice(h->device));
+  return PETDIFF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* petdiff_last_error(void) { return g_err.c_str(); }
+
+int petdiff_default_config(petdiff_config* c) {
+  if (!c) return fail(PETDIFF_ERR_INVALID, "null config");
+  c->n_roi = 48;
+  c->n_par = 2;
+  c->n_frames = 54;
+  c->n_cond_rows = 49;
+  c->num_filt_start = 128;
+  c->depth = 4;
+  c->kernel_size = 6;
+  c->pool_size = 2;
+  c->sin_emb_dim = 64;
+  c->enc_size[0] = 256;
+  c->enc_size[1] = 128;
+  c->enc_size[2] = 64;
+  c->latent_dim = 32;
+  c->timesteps = 1000;
+  c->learn_variance = PETDIFF_LEARN_RANGED;
+  c->parameterization = PETDIFF_PARAM_EPS;
+  c->dtype = PETDIFF_DTYPE_BF16;
+  return PETDIFF_OK;
+}
+
+size_t petdiff_param_count(const petdiff_config* c) {
+  if (!c) return 0;
+  const int n_out = c->learn_variance == PETDIFF_LEARN_FIXED ? c->n_par : 2 * c->n_par;
+  const auto s = make_spec(*c, n_out);
+  return s.back().off + s.back().size;
+}
+
+int petdiff_cosine_schedule(int T, double offset_s, double max_beta, float* beta_out) {
+  if (T <= 0 || !beta_out) return fail(PETDIFF_ERR_INVALID, "bad arguments");
+  const double pi = 3.141592653589793;
+  for (int i = 0; i < T; ++i) {
+    const double t1 = (double)i / T, t2 = (double)(i + 1) / T;
+    const float a1 = cosf((float)((t1 + offset_s) / (1 + offset_s) * pi / 2));
+    const float a2 = cosf((float)((t2 + offset_s) / (1 + offset_s) * pi / 2));
+    const float ab1 = a1 * a1, ab2 = a2 * a2;
+    const float b = 1.0f - ab2 / ab1;
+    beta_out[i] = (double)b < max_beta ? b : (float)max_beta;
+  }
+  return PETDIFF_OK;
+}
+
+int petdiff_create(const petdiff_config* cfg, const float* weights, size_t n_weights, int device,
+                   petdiff_handle* out) {
+  if (!cfg || !weights || !out) return fail(PETDIFF_ERR_INVALID, "null argument");
+  if (!is_shipped_arch(*cfg))
+    return fail(PETDIFF_ERR_UNSUPPORTED,
+                "only the shipped UnetConditional (f128/d4, k6, L48, enc 256-128-64-32) is compiled");
+  if (cfg->dtype != PETDIFF_DTYPE_F32 && cfg->dtype != PETDIFF_DTYPE_BF16)
+    return fail(PETDIFF_ERR_INVALID, "dtype must be PETDIFF_DTYPE_F32 or PETDIFF_DTYPE_BF16");
+  if (cfg->learn_variance < 0 || cfg->learn_variance > 2 || cfg->parameterization < 0 ||
+      cfg->parameterization > 3)
+    return fail(PETDIFF_ERR_INVALID, "bad learn_variance / parameterization");
+  std::unique_ptr<petdiff_ctx> h(new petdiff_ctx());
+  h->cfg = *cfg;
+  h->device = device;
+  h->n_out = cfg->learn_variance == PETDIFF_LEARN_FIXED ? cfg->n_par : 2 * cfg->n_par;
+  h->spec = make_spec(*cfg, h->n_out);
+  const size_t need = h->spec.back().off + h->spec.back().size;
+  if (n_weights != need)
+    return fail(PETDIFF_ERR_INVALID, "weight blob has " + std::to_string(n_weights) + " values, expected " +
+                                         std::to_string(need));
+  for (auto& s : h->spec) h->off[s.name] = s.off;
+  HIPC(hipSetDevice(device));
+  HIPC(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
+  HIPC(h->w32.alloc(need * 4));
+  HIPC(hipMemcpy(h->w32.p, weights, need * 4, hipMemcpyHostToDevice));
+  std::vector<float> host(weights, weights + need);
+  for (int li = 0; li < kNumConvLayers; ++li) {
+    if (cfg->dtype == PETDIFF_DTYPE_BF16) CHK((pack_conv<bf16, uint16_t>(h.get(), host, li)));
+    else CHK((pack_conv<float, float>(h.get(), host, li)));
+    const ConvLayer& cl = kConv[li];
+    if (cl.cond_level < 0) {
+      std::vector<float> b(cl.cout);
+      const float* bc = host.data() + h->off.at(std::string(cl.wname) + ".bias");
+      const float* br = host.data() + h->off.at(std::string(cl.resname) + ".bias");
+      for (int n = 0; n < cl.cout; ++n) b[n] = bc[n] + br[n];
+      HIPC(h->bias_only[li].alloc(cl.cout * 4));
+      HIPC(hipMemcpy(h->bias_only[li].p, b.data(), cl.cout * 4, hipMemcpyHostToDevice));
+    }
+  }
+  // down0: x channels 50, 51 of down0.conv (6, 52, 128) with the res kernel folded into tap 2
+  {
+    std::vector<float> w0(6 * 2 * 128);
+    const float* wk = host.data() + h->off.at("down0.conv.kernel");
+    const float* wr = host.data() + h->off.at("down0.res.kernel");
+    for (int j = 0; j < 6; ++j)
+      for (int c = 0; c < 2; ++c)
+        for (int n = 0; n < 128; ++n) {
+          float v = wk[((size_t)j * 52 + 50 + c) * 128 + n];
+          if (j == 2) v += wr[(size_t)(50 + c) * 128 + n];
+          w0[(j * 2 + c) * 128 + n] = v;
+        }
+    HIPC(h->w0.alloc(w0.size() * 4));
+    HIPC(hipMemcpy(h->w0.p, w0.data(), w0.size() * 4, hipMemcpyHostToDevice));
+  }
+  *out = h.release();
+  return PETDIFF_OK;
+}
+
+int petdiff_destroy(petdiff_handle h) {
+  if (!h) return PETDIFF_OK;
+  (void)hipSetDevice(h->device);
+  (void)hipDeviceSynchronize();
+  for (auto& kv : h->graphs) {
+    if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+    if (kv.second.graph) (void)hipGraphDestroy(kv.second.graph);
+  }
+  for (auto e : h->ev_pool) (void)hipEventDestroy(e);
+  if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
+  delete h;
+  return PETDIFF_OK;
+}
+
+int petdiff_set_schedule(petdiff_handle h, const float* tables, int T) {
+  CHK(valid_handle(h));
+  if (!tables || T <= 0) return fail(PETDIFF_ERR_INVALID, "bad schedule tables");
+  HIPC(h->tab.alloc((size_t)kNTab * T * 4));
+  HIPC(hipMemcpy(h->tab.p, tables, (size_t)kNTab * T * 4, hipMemcpyHostToDevice));
+  h->T = T;
+  // time path: SinusoidalPosEmb -> Dense(48) -> GELU for every t, then each
+  // level's Dense(L) and its folded conv contribution (+ the conv biases).
+  HIPC(h->temb.alloc((size_t)T * h->cfg.n_roi * 4));
+  HIPC(h->tseq.alloc((size_t)T * 48 * 4));
+  HIPC(launch_time_emb(h->W("time_mlp.kernel"), h->W("time_mlp.bias"), T, h->cfg.sin_emb_dim, h->cfg.n_roi,
+                       h->temb.as<float>(), 0));
+  for (int lv = 0; lv < 7; ++lv) {
+    const CondLevel& c = kLevels[lv];
+    const std::string p = c.prefix;
+    HIPC(launch_dense(h->temb.as<float>(), T, h->cfg.n_roi, h->W(p + ".time_proj.kernel"),
+                      h->W(p + ".time_proj.bias"), c.Lseq, 0, h->tseq.as<float>(), 0));
+    HIPC(h->tmap[lv].alloc((size_t)T * c.Lout * c.cout * 4));
+    const std::string cv = p + "." + c.conv;
+    HIPC(launch_fold(h->tseq.as<float>(), T, c.Lseq, 1, h->W(cv + ".kernel"), c.taps, c.padl, c.ups, c.cin_full,
+                     h->cfg.n_cond_rows, c.res ? h->W(p + ".res.kernel") : nullptr, h->W(cv + ".bias"),
+                     c.res ? h->W(p + ".res.bias") : nullptr, h->tmap[lv].as<float>(), c.Lout, c.cout, 0));
+  }
+  HIPC(hipDeviceSynchronize());
+  h->sched_set = true;
+  return PETDIFF_OK;
+}
+
+int petdiff_set_conditions(petdiff_handle h, const float* cond, int n_tac, void* stream) {
+  CHK(valid_handle(h));
+  if (!cond || n_tac <= 0) return fail(PETDIFF_ERR_INVALID, "bad conditions");
+  hipStream_t s = (hipStream_t)stream;
+  const int rows = n_tac * h->cfg.n_cond_rows;
+  HIPC(h->enc_a.alloc((size_t)rows * 256 * 4));
+  HIPC(h->enc_b.alloc((size_t)rows * 256 * 4));
+  float* A = h->enc_a.as<float>();
+  float* Bf = h->enc_b.as<float>();
+  // Encoder_v3_noskip (networks.py:574-586): 54-256-128-64 relu, -> 32 linear
+  HIPC(launch_dense(cond, rows, 54, h->W("cond_enc.hidden0.kernel"), h->W("cond_enc.hidden0.bias"), 256, 1, A, s));
+  HIPC(launch_dense(A, rows, 256, h->W("cond_enc.hidden1.kernel"), h->W("cond_enc.hidden1.bias"), 128, 1, Bf, s));
+  HIPC(launch_dense(Bf, rows, 128, h->W("cond_enc.hidden2.kernel"), h->W("cond_enc.hidden2.bias"), 64, 1, A, s));
+  HIPC(launch_dense(A, rows, 64, h->W("cond_enc.z.kernel"), h->W("cond_enc.z.bias"), 32, 0, Bf, s));
+  for (int lv = 0; lv < 7; ++lv) {
+    const CondLevel& c = kLevels[lv];
+    const std::string p = c.prefix;
+    // label projection Dense(L) on (n_tac*49, 32) -> flat (n_tac, 49*L) == raw Reshape((L, 49))
+    HIPC(launch_dense(Bf, rows, 32, h->W(p + ".label_proj.kernel"), h->W(p + ".label_proj.bias"), c.Lseq, 0, A, s));
+    HIPC(h->cmap[lv].alloc((size_t)n_tac * c.Lout * c.cout * 4));
+    const std::string cv = p + "." + c.conv;
+    HIPC(launch_fold(A, n_tac, c.Lseq, h->cfg.n_cond_rows, h->W(cv + ".kernel"), c.taps, c.padl, c.ups,
+                     c.cin_full, 0, c.res ? h->W(p + ".res.kernel") : nullptr, nullptr, nullptr,
+                     h->cmap[lv].as<float>(), c.Lout, c.cout, s));
+  }
+  if (n_tac != h->n_tac) {
+    for (auto& kv : h->graphs) {
+      if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+      if (kv.second.graph) (void)hipGraphDestroy(kv.second.graph);
+    }
+    h->graphs.clear();
+  }
+  h->n_tac = n_tac;
+  return PETDIFF_OK;
+}
+
+int petdiff_forward(petdiff_handle h, const float* x, const int32_t* t, const int32_t* tac, float* out, int B,
+                    void* stream) {
+  CHK(valid_handle(h));
+  if (B < 0 || (B > 0 && (!x || !t || !out))) return fail(PETDIFF_ERR_INVALID, "bad arguments");
+  if (B == 0) return PETDIFF_OK;
+  CHK(ensure_workspace(h, B));
+  StepIO io{};
+  io.x_in = x;
+  io.t_uniform = -1;
+  io.tvec = t;
+  io.tac = tac;
+  io.fin = base_final(h);
+  io.fin.x_t = x;
+  io.fin.net_out = out;
+  return network(h, io, B, (hipStream_t)stream);
+}
+
+int petdiff_p_sample(petdiff_handle h, const float* x, const int32_t* t, const int32_t* tac, const float* z,
+                     uint64_t seed, uint64_t sample_offset, int rng_step, float* mean, float* var,
+                     float* var_tilde, int B, void* stream) {
+  CHK(valid_handle(h));
+  if (B < 0 || (B > 0 && (!x || !t))) return fail(PETDIFF_ERR_INVALID, "bad arguments");
+  if (B == 0) return PETDIFF_OK;
+  CHK(ensure_workspace(h, B));
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned long long rp[2] = {seed, sample_offset};
+  HIPC(hipMemcpyAsync(h->rng.p, rp, 16, hipMemcpyHostToDevice, s));
+  StepIO io{};
+  io.x_in = x;
+  io.t_uniform = -1;
+  io.tvec = t;
+  io.tac = tac;
+  io.fin = base_final(h);
+  io.fin.x_t = x;
+  io.fin.z = z;
+  io.fin.rng_step = rng_step;
+  io.fin.mean_out = mean;
+  io.fin.var_out = var;
+  io.fin.var_tilde_out = var_tilde;
+  CHK(network(h, io, B, s));
+  HIPC(hipStreamSynchronize(s));   // rp lives on this stack frame
+  return PETDIFF_OK;
+}
+
+int petdiff_generate(petdiff_handle h, const float* x_T, const int32_t* tac, const int32_t* t_seq, int n_steps,
+                     int flag_var_tilde, const float* z_all, uint64_t seed, uint64_t sample_offset, float* x_out,
+                     float* all_xt, int B, int use_graph, void* stream) {
+  CHK(valid_handle(h));
+  if (B < 0 || n_steps < 0 || (B > 0 && (!x_T || !x_out)) || (n_steps > 0 && !t_seq))
+    return fail(PETDIFF_ERR_INVALID, "bad arguments");
+  if (B == 0) return PETDIFF_OK;
+  for (int i = 0; i < n_steps; ++i)
+    if (t_seq[i] < 0 || t_seq[i] >= h->T) return fail(PETDIFF_ERR_INVALID, "timestep index out of range");
+  CHK(ensure_workspace(h, B));
+  hipStream_t s = (hipStream_t)stream;
+  const size_t xbytes = (size_t)B * h->cfg.n_roi * h->cfg.n_par * 4;
+  static thread_local unsigned long long rp[2];
+  rp[0] = seed;
+  rp[1] = sample_offset;
+  HIPC(hipMemcpyAsync(h->rng.p, rp, 16, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(h->xa.p, x_T, xbytes, hipMemcpyDeviceToDevice, s));
+  const int* tacp = nullptr;
+  if (tac) {
+    HIPC(hipMemcpyAsync(h->tacbuf.p, tac, (size_t)B * 4, hipMemcpyDeviceToDevice, s));
+    tacp = h->tacbuf.as<int>();
+  }
+  float* bufs[2] = {h->xa.as<float>(), h->xb.as<float>()};
+  auto enqueue = [&](hipStream_t q) -> int {
+    for (int i = 0; i < n_steps; ++i) {
+      StepIO io{};
+      io.x_in = bufs[i & 1];
+      io.t_uniform = t_seq[i];
+      io.tvec = nullptr;
+      io.tac = tacp;
+      io.fin = base_final(h);
+      io.fin.x_t = bufs[i & 1];
+      io.fin.z = z_all ? z_all + (size_t)i * B * 96 : nullptr;
+      io.fin.rng_step = i;
+      io.fin.flag_var_tilde = flag_var_tilde;
+      io.fin.x_next = bufs[(i + 1) & 1];
+      io.fin.x_all = all_xt ? all_xt + (size_t)i * B * 96 : nullptr;
+      CHK(network(h, io, B, q));
+    }
+    return PETDIFF_OK;
+  };
+  const bool graph = use_graph && !z_all && !all_xt && !h->timing && n_steps > 0;
+  if (!graph) {
+    CHK(enqueue(s));
+  } else {
+    std::vector<int> key{B, flag_var_tilde, tac ? 1 : 0, n_steps};
+    key.insert(key.end(), t_seq, t_seq + n_steps);
+    auto it = h->graphs.find(key);
+    if (it == h->graphs.end()) {
+      GraphEntry ge;
+      HIPC(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
+      int rc = enqueue(h->cap_stream);
+      hipGraph_t g = nullptr;
+      hipError_t ee = hipStreamEndCapture(h->cap_stream, &g);
+      if (rc != PETDIFF_OK) {
+        if (g) (void)hipGraphDestroy(g);
+        return rc;
+      }
+      HIPC(ee);
+      ge.graph = g;
+      HIPC(hipGraphInstantiate(&ge.exec, g, nullptr, nullptr, 0));
+      it = h->graphs.emplace(key, ge).first;
+    }
+    HIPC(hipGraphLaunch(it->second.exec, s));
+  }
+  HIPC(hipMemcpyAsync(x_out, bufs[n_steps & 1], xbytes, hipMemcpyDeviceToDevice, s));
+  return PETDIFF_OK;
+}
+
+int petdiff_posterior_stats(petdiff_handle h, const float* x0, const int32_t* tac, int B, int n_tac,
+                            double* stats, void* stream) {
+  CHK(valid_handle(h));
+  if (!x0 || !stats || B < 0 || n_tac <= 0) return fail(PETDIFF_ERR_INVALID, "bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  const int ncol = h->cfg.n_roi * h->cfg.n_par;
+  DevBuf d;
+  HIPC(d.alloc((size_t)n_tac * ncol * 3 * 8));
+  HIPC(launch_posterior_stats(x0, tac, B, n_tac, ncol, d.as<double>(), s));
+  HIPC(hipMemcpyAsync(stats, d.p, (size_t)n_tac * ncol * 3 * 8, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  return PETDIFF_OK;
+}
+
+int petdiff_set_timing(petdiff_handle h, int enable) {
+  CHK(valid_handle(h));
+  h->timing = enable != 0;
+  return PETDIFF_OK;
+}
+
+int petdiff_get_timing(petdiff_handle h, float* total_ms, int* count) {
+  CHK(valid_handle(h));
+  for (int i = 0; i < PETDIFF_NUM_LAYERS; ++i) {
+    if (total_ms) total_ms[i] = 0.f;
+    if (count) count[i] = 0;
+  }
+  for (auto& u : h->ev_used) {
+    HIPC(hipEventSynchronize(u.second.second));
+    float ms = 0.f;
+    HIPC(hipEventElapsedTime(&ms, u.second.first, u.second.second));
+    if (total_ms) total_ms[u.first] += ms;
+    if (count) count[u.first] += 1;
+  }
+  h->ev_used.clear();
+  h->ev_next = 0;
+  return PETDIFF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,104 @@
+// Internal declarations shared by the HIP kernels (unet_kernels.hip) and the
+// C-ABI host implementation (petdiff_api.cpp).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstddef>
+
+namespace petdiff {
+
+typedef __bf16 bf16;
+
+// Tile geometry of the implicit-GEMM Conv1D kernel (see DESIGN.md "conv kernel").
+constexpr int kMT = 192;      // output rows (sample x position) per workgroup
+constexpr int kNT = 128;      // output channels per workgroup
+constexpr int kRowB = 64;     // bytes of one LDS row chunk (32 bf16 / 16 f32 channels)
+constexpr int kThreads = 256; // 4 waves: 2 (M) x 2 (N), 96 x 64 per wave
+
+// Epilogue kinds
+enum Epi : int {
+  EPI_POOL = 0,   // relu, write skip + maxpool(2) output       (down blocks 1,2)
+  EPI_RELU = 1,   // relu, write                                (down3, up blocks 0,1)
+  EPI_LIN = 2,    // linear, write                              (up-sampling conv2)
+  EPI_FINAL = 3,  // relu -> LDS -> final 1x1 conv -> p_sample  (up block 2)
+};
+
+// Per-timestep fp32 tables, row k of a [kNTab][T] array (computed on the host
+// exactly like diffusion_model.py:98-105, 337-355; see petdiff.h).
+enum Tab : int {
+  TAB_BETA = 0, TAB_LOG_BETA, TAB_PLVC, TAB_POST_VAR, TAB_C1, TAB_C2, TAB_ALPHA_BAR,
+  TAB_SQRT_AB, TAB_SQRT_1M_AB, TAB_INV_SQRT_AB, TAB_SQRT_RECIP_M1, TAB_RECIP_C1,
+  TAB_C2_OVER_C1, kNTab
+};
+
+struct FinalArgs {
+  const float* wf;     // [128][n_out] final Conv1D 1x1 kernel
+  const float* bf;     // [n_out]
+  int n_out;           // 4 (learned variance) or 2
+  const float* x_t;    // [B][n_roi][2] current sample
+  const float* z;      // injected noise [B][n_roi][2] or null -> Philox
+  const unsigned long long* rng;  // device {seed, sample_offset}
+  int rng_step;
+  const float* tab;    // [kNTab][T]
+  int T;
+  int learn_mode;      // 0 fixed, 1 learn, 2 learn_ranged
+  int param_mode;      // 0 eps, 1 x0, 2 v, 3 x_prev
+  int flag_var_tilde;
+  float* x_next;       // mean + noise (loop mode) or null
+  float* x_all;        // keep_all_xt slot for this step or null
+  float* mean_out;     // p_sample outputs or null
+  float* var_out;
+  float* var_tilde_out;
+  float* net_out;      // raw network output [B][n_roi][n_out] or null (then no p_sample)
+};
+
+template <typename T>
+struct ConvArgs {
+  const T* src1; int c1;     // first input (channels-last rows)
+  const T* src2; int c2;     // second input (concat [src1 | src2]) or null
+  const T* wpack;            // packed weights [Cout/128][NC][taps][128][4 x 16B]
+  T* out;                    // [B*L][cout]
+  T* out_pool;               // [B*L/2][cout] (EPI_POOL)
+  const float* cmap;         // [n_tac][L][cout] label contribution or null
+  const float* tmap;         // [T][L][cout] time contribution + biases, or null
+  const float* bias;         // [cout] when tmap is null
+  const int* tac;            // [B] condition index per sample (null -> 0)
+  const int* tvec;           // [B] timestep per sample (used when t_uniform < 0)
+  int t_uniform;
+  int B, cout;
+  FinalArgs fin;
+};
+
+struct Down0Args {
+  const float* x;            // [B][48][2]
+  const float* w0;           // [6][2][128], residual folded into tap 2
+  const float* cmap;         // [n_tac][48][128]
+  const float* tmap;         // [T][48][128]
+  const int* tac; const int* tvec; int t_uniform;
+  void* s0; void* p0;        // T*
+  int B;
+};
+
+// Launch helpers (unet_kernels.hip).  Return hipError_t.
+template <typename T>
+hipError_t launch_conv(int layer_kind, const ConvArgs<T>& a, hipStream_t s);
+template <typename T>
+hipError_t launch_down0(const Down0Args& a, hipStream_t s);
+
+hipError_t launch_time_emb(const float* w, const float* b, int T, int sin_dim, int hid, float* out,
+                           hipStream_t s);
+hipError_t launch_dense(const float* in, int rows, int din, const float* w, const float* b, int dout,
+                        int act, float* out, hipStream_t s);
+hipError_t launch_fold(const float* seq, int n, int Lseq, int Cs, const float* wk, int taps, int padl,
+                       int ups, int cin_full, int ch0, const float* wr, const float* b1,
+                       const float* b2, float* out, int Lout, int cout, hipStream_t s);
+hipError_t launch_posterior_stats(const float* x0, const int* tac, int B, int n_tac, int ncol,
+                                  double* stats, hipStream_t s);
+
+// Layer kinds of launch_conv (fixed shapes of the shipped config).
+enum LayerKind : int {
+  LK_DOWN1 = 0, LK_DOWN2, LK_DOWN3, LK_UP0_CONV2, LK_UP0_BLOCK, LK_UP1_CONV2, LK_UP1_BLOCK,
+  LK_UP2_CONV2, LK_UP2_BLOCK, kNumConvLayers
+};
+
+}  // namespace petdiff

@@ -1,0 +1,341 @@
+"""Drop-in ``ImprovedDDPM`` sampling API backed by libpetdiff.so (gfx950 HIP).
+
+Mirrors the public sampling surface of the reference's diffusion_model.py
+(yanisdjebra/PET_posterior_distribution):
+
+=====================================  ===========================================
+reference (file:line)                  here
+=====================================  ===========================================
+DDPM.__init__ schedule  :85-105        ``ImprovedDDPM.__init__`` (same attributes)
+ImprovedDDPM.__init__   :319-357       same (+ ValueError on bad parameterization)
+DDPM.call               :141-158       ``call`` / ``__call__`` -> petdiff_forward
+ImprovedDDPM.ddpm       :651-663       ``ddpm`` (= ``p_sample``) -> petdiff_p_sample
+tfunc_ddpm              :665-668       ``tfunc_ddpm``
+ddpm_loop               :670-715       ``ddpm_loop`` (= ``generate``) -> petdiff_generate
+tfunc_ddpm_loop         :718-737       ``tfunc_ddpm_loop`` (hipGraph replay)
+=====================================  ===========================================
+
+Inputs may be NumPy arrays or torch tensors; outputs are torch tensors on the
+sampler's GPU (``keep_all_xt`` returns a NumPy stack, as the reference does at
+:712-713).  The network runs in ``dtype`` ('bfloat16' by default, or 'float32'
+for the exact-f32 MFMA parity mode); the p_sample epilogue is always fp32.
+
+Noise: the reference draws ``tf.random.normal`` from TF's stateful Philox.  Here
+z is a counter-based Philox4x32-10 normal keyed by (seed, global sample index,
+loop step), so results do not depend on batch chunking or on how samples are
+sharded over GPUs.  ``z=`` injects explicit noise (used by the parity tests).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+from .helper_func import NP_DTYPE, get_beta_schedule
+
+DTYPE = 'float32'   # dtype of every host-side table and of x (diffusion_model.py:7)
+
+
+def _as_device(x, device, dtype):
+    if isinstance(x, torch.Tensor):
+        return x.to(device=device, dtype=dtype).contiguous()
+    return torch.as_tensor(np.asarray(x), dtype=dtype, device=device).contiguous()
+
+
+def _stream_ptr(device):
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class ImprovedDDPM:
+    """iDDPM posterior sampler (diffusion_model.py:317-748, sampling part)."""
+
+    eps_param_name_list = ['eps', 'epsilon']
+    x0_param_name_list = ['x0', 'x_0', 'x_start', 'xstart', 'start_x']
+    x_prev_param_name_list = ['x_{t-1}', 'x_prev', 'xprev', 'prev_x']
+    v_param_name_list = ['v', ]
+
+    def __init__(self, lambda_vlb=0.1, parameterization='eps', timesteps=200, noise_schedule=None,
+                 network=None, ndim=None, constrained_func_output_t0=None, dtype='bfloat16', device=None,
+                 seed=12345, **kwargs):
+        # ---- DDPM.__init__ (diffusion_model.py:79-135) ----
+        self.timesteps = timesteps
+        self.noise_schedule = noise_schedule
+        self.constrained_func_output_t0 = constrained_func_output_t0
+        if constrained_func_output_t0 is not None:
+            raise NotImplementedError('constrained_func_output_t0 is not supported by the fused kernel')
+        ns = noise_schedule or {}
+        self.beta_start = ns.get('beta_start', 1e-4)
+        self.beta_end = ns.get('beta_end', 2e-2)
+        self.offset_s = ns.get('offset_s', 0.008)
+        self.max_beta = ns.get('max_beta', 0.999)
+        self.schedule_name = ns.get('schedule_name', 'linear') if noise_schedule is not None else 'linear'
+        self.beta = get_beta_schedule(self.schedule_name, self.timesteps, beta_start=self.beta_start,
+                                      beta_end=self.beta_end, offset_s=self.offset_s, max_beta=self.max_beta)
+        self.alpha = 1 - self.beta
+        if network is None:
+            raise ValueError('Input network is required to create model.')
+        self.network = network
+        if ndim is not None:
+            self.ndim = ndim
+        elif getattr(network, 'ndim', None) is not None:
+            self.ndim = network.ndim
+        elif hasattr(network, 'input_shape'):
+            self.ndim = len(network.input_shape) - 2
+        else:
+            raise AttributeError('``ndim`` was not passed as argument. Could not be retrieved from input '
+                                 'network {} (``input_shape`` attribute does not exist).'.format(
+                                     type(network).__name__))
+        self.reshape_dim = (-1,) + (1,) * (self.ndim + 1)
+        self.flag_condition = True
+        # ---- ImprovedDDPM.__init__ (diffusion_model.py:319-355) ----
+        self.lambda_vlb = lambda_vlb
+        self.parameterization = parameterization
+        self.all_param_name_list = (self.eps_param_name_list + self.x0_param_name_list +
+                                    self.x_prev_param_name_list + self.v_param_name_list)
+        if self.parameterization.lower() not in self.all_param_name_list:
+            raise ValueError(f'Invalid parameterization (got ``{parameterization}``). '
+                             f'Value must be in ``{self.all_param_name_list}``')
+        self.learn_variance = network.learn_variance
+        self.flag_learn_var = 'learn' in self.learn_variance.lower()
+        self.flag_ranged_var = 'ranged' in self.learn_variance.lower()
+        self.alpha_bar = np.cumprod(self.alpha, 0, dtype=DTYPE)
+        self.alpha_bar_prev = np.concatenate((np.array([1.], dtype=DTYPE), self.alpha_bar[:-1]), axis=0)
+        self.sqrt_alpha_bar = np.sqrt(self.alpha_bar, dtype=DTYPE)
+        self.sqrt_one_minus_alpha_bar = np.sqrt(1 - self.alpha_bar, dtype=DTYPE)
+        self.posterior_variance = self.beta * (1.0 - self.alpha_bar_prev) / (1.0 - self.alpha_bar)
+        # the reference's alias (:349-351): element 0 of posterior_variance is overwritten too
+        self.posterior_log_variance_clipped = self.posterior_variance
+        self.posterior_log_variance_clipped[0] = self.posterior_log_variance_clipped[1]
+        self.posterior_log_variance_clipped = np.log(self.posterior_log_variance_clipped)
+        self.posterior_mean_coef1 = self.beta * np.sqrt(self.alpha_bar_prev) / (1.0 - self.alpha_bar)
+        self.posterior_mean_coef2 = (1.0 - self.alpha_bar_prev) * np.sqrt(self.alpha) / (1.0 - self.alpha_bar)
+
+        self.dtype = {'bfloat16': _lib.DTYPE_BF16, 'bf16': _lib.DTYPE_BF16,
+                      'float32': _lib.DTYPE_F32, 'fp32': _lib.DTYPE_F32}[str(dtype)]
+        if device is None:
+            device = torch.cuda.current_device() if torch.cuda.is_available() else 0
+        self.device = torch.device('cuda', device if isinstance(device, int) else torch.device(device).index or 0)
+        self.seed = int(seed)
+        self._call_counter = 0
+        self._handle = None
+        self._cond_cache = None     # (unique-conditions tensor) last sent to the library
+        self.name = 'improved_ddpm'
+
+    # ------------------------------------------------------------------ setup
+    def schedule_tables(self):
+        """[NTAB][T] fp32 tables (row order of include/petdiff.h), all NumPy float32 ops."""
+        one = NP_DTYPE(1.0)
+        c1, c2 = self.posterior_mean_coef1, self.posterior_mean_coef2
+        rows = [self.beta, np.log(self.beta), self.posterior_log_variance_clipped, self.posterior_variance,
+                c1, c2, self.alpha_bar, self.sqrt_alpha_bar, self.sqrt_one_minus_alpha_bar,
+                one / self.sqrt_alpha_bar, np.sqrt(one / self.alpha_bar - one),
+                1.0 / c1, c2 / c1]
+        return np.ascontiguousarray(np.stack([np.asarray(r, dtype=NP_DTYPE) for r in rows]))
+
+    def _ensure_handle(self):
+        if self._handle is not None:
+            return self._handle
+        L = _lib.lib()
+        if self.network.weights is None:
+            self.network.build((None, 48, 2))
+        cfg = _lib.PetdiffConfig()
+        _lib.check(L.petdiff_default_config(C.byref(cfg)))
+        cfg.timesteps = self.timesteps
+        lv = self.learn_variance.lower()
+        cfg.learn_variance = (_lib.LEARN_RANGED if 'ranged' in lv else _lib.LEARN) if 'learn' in lv \
+            else _lib.LEARN_FIXED
+        p = self.parameterization.lower()
+        cfg.parameterization = (_lib.PARAM_XPREV if p in self.x_prev_param_name_list else
+                                _lib.PARAM_X0 if p in self.x0_param_name_list else
+                                _lib.PARAM_V if p in self.v_param_name_list else _lib.PARAM_EPS)
+        cfg.dtype = self.dtype
+        blob = self.network.flat_weights()
+        h = C.c_void_p()
+        torch.cuda.set_device(self.device)
+        _lib.check(L.petdiff_create(C.byref(cfg), blob.ctypes.data_as(C.c_void_p), blob.size, self.device.index,
+                                    C.byref(h)), 'petdiff_create')
+        self._handle = h
+        tabs = self.schedule_tables()
+        _lib.check(L.petdiff_set_schedule(h, tabs.ctypes.data_as(C.c_void_p), self.timesteps),
+                   'petdiff_set_schedule')
+        return h
+
+    def load_weights(self, path):
+        self.network.load_weights(path)
+        self.close()
+
+    def close(self):
+        if self._handle is not None:
+            _lib.lib().petdiff_destroy(self._handle)
+            self._handle = None
+            self._cond_cache = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _conditions(self, condition, B):
+        """Deduplicate conditions -> (per-sample index tensor or None).
+
+        The reference feeds np.repeat(y_obs, B) (main_script.py:419); the kernels
+        fold each UNIQUE condition once (encoder + label maps) and index it per sample.
+        """
+        h = self._ensure_handle()
+        if condition is None:
+            raise NotImplementedError('the shipped UnetConditional requires a condition')
+        cond = _as_device(condition, self.device, torch.float32)
+        if cond.dim() == 2:
+            cond = cond[None]
+        if cond.shape[1:] != (49, 54):
+            raise ValueError(f'condition must be (B, 49, 54), got {tuple(cond.shape)}')
+        if cond.shape[0] != B and cond.shape[0] != 1:
+            raise ValueError(f'condition batch {cond.shape[0]} != x batch {B}')
+        if cond.shape[0] == 1 or bool((cond == cond[:1]).all()):
+            uniq, inv = cond[:1].contiguous(), None
+        else:
+            uniq, inv = torch.unique(cond.reshape(cond.shape[0], -1), dim=0, return_inverse=True)
+            uniq = uniq.reshape(-1, 49, 54).contiguous()
+            inv = inv.to(torch.int32).contiguous()
+        if self._cond_cache is None or self._cond_cache.shape != uniq.shape or \
+                not torch.equal(self._cond_cache, uniq):
+            _lib.check(_lib.lib().petdiff_set_conditions(h, _ptr(uniq), uniq.shape[0], _stream_ptr(self.device)),
+                       'petdiff_set_conditions')
+            self._cond_cache = uniq
+        return inv, uniq.shape[0]
+
+    def _time(self, time, B):
+        t = _as_device(time, self.device, torch.int32).reshape(-1)
+        if t.numel() == 1 and B != 1:
+            t = t.expand(B).contiguous()
+        if t.numel() != B:
+            raise ValueError('time must have one entry per sample')
+        if B and (int(t.min()) < 0 or int(t.max()) >= self.timesteps):
+            raise ValueError(f'time must be in [0, {self.timesteps})')
+        return t
+
+    # ------------------------------------------------------------------ API
+    def call(self, inputs, training=False, **kwargs):
+        """DDPM.call (diffusion_model.py:141-158): raw network output (B, 48, n_out)."""
+        x = _as_device(inputs['x'], self.device, torch.float32)
+        B = x.shape[0]
+        t = self._time(inputs.get('time'), B)
+        tac, _ = self._conditions(inputs.get('condition'), B)
+        out = torch.empty((B, x.shape[1], self.network.n_out), dtype=torch.float32, device=self.device)
+        _lib.check(_lib.lib().petdiff_forward(self._handle, _ptr(x), _ptr(t), _ptr(tac), _ptr(out), B,
+                                              _stream_ptr(self.device)), 'petdiff_forward')
+        return out
+
+    __call__ = call
+
+    def ddpm(self, x_t, time, condition=None, z=None, seed=None, sample_offset=0, rng_step=None):
+        """ImprovedDDPM.ddpm = p_sample (diffusion_model.py:651-663) -> (mean, var, var_tilde)."""
+        x = _as_device(x_t, self.device, torch.float32)
+        B = x.shape[0]
+        t = self._time(time, B)
+        tac, _ = self._conditions(condition, B)
+        zt = None if z is None else _as_device(z, self.device, torch.float32)
+        if zt is not None and zt.shape != x.shape:
+            raise ValueError('z must have the shape of x_t')
+        if rng_step is None:
+            rng_step = self._call_counter
+            self._call_counter += 1
+        mean = torch.empty_like(x)
+        var = torch.empty_like(x)
+        var_tilde = torch.empty_like(x)
+        _lib.check(_lib.lib().petdiff_p_sample(
+            self._handle, _ptr(x), _ptr(t), _ptr(tac), _ptr(zt), self.seed if seed is None else int(seed),
+            int(sample_offset), int(rng_step), _ptr(mean), _ptr(var), _ptr(var_tilde), B,
+            _stream_ptr(self.device)), 'petdiff_p_sample')
+        return mean, var, var_tilde
+
+    p_sample = ddpm
+
+    def tfunc_ddpm(self, x_t, time, condition=None, **kwargs):
+        """diffusion_model.py:665-668."""
+        return self.ddpm(x_t, time, condition, **kwargs)
+
+    def sub_sequence(self, num_timesteps=None, sub_sequence_type='linear'):
+        """Index list of ddpm_loop (diffusion_model.py:680-691, same substring semantics)."""
+        if num_timesteps in (None, 0, self.timesteps):
+            return list(range(self.timesteps))[::-1]
+        if sub_sequence_type in 'linear':
+            return np.linspace(0, self.timesteps - 1, num=num_timesteps, dtype=np.int32)[::-1].tolist()
+        if sub_sequence_type in 'quadratic':
+            return (np.linspace(0, np.sqrt(self.timesteps - 1), num=num_timesteps,
+                                dtype=np.int32)[::-1] ** 2).tolist()
+        raise ValueError('Subsequence type not recognized (given {})'.format(sub_sequence_type))
+
+    def ddpm_loop(self, x_T, condition, num_timesteps=None, sub_sequence_type='linear', flag_var_tilde=True,
+                  keep_all_xt=False, z=None, seed=None, sample_offset=0, use_graph=True):
+        """ImprovedDDPM.ddpm_loop = generate (diffusion_model.py:670-715).
+
+        Extra keywords: ``z`` injected noise (n_steps, B, 48, 2); ``seed`` /
+        ``sample_offset`` select the counter-based noise stream (global index of
+        sample b is sample_offset + b); ``use_graph`` replays the whole loop as one
+        captured hipGraph.
+        """
+        indices = self.sub_sequence(num_timesteps, sub_sequence_type)
+        x = _as_device(x_T, self.device, torch.float32)
+        B = x.shape[0]
+        tac, _ = self._conditions(condition, B)
+        n = len(indices)
+        zt = None if z is None else _as_device(z, self.device, torch.float32)
+        if zt is not None and tuple(zt.shape) != (n,) + tuple(x.shape):
+            raise ValueError('z must be (n_steps,) + x_T.shape')
+        all_xt = torch.empty((n,) + tuple(x.shape), dtype=torch.float32, device=self.device) \
+            if keep_all_xt else None
+        out = torch.empty_like(x)
+        tseq = np.ascontiguousarray(np.asarray(indices, dtype=np.int32))
+        if seed is None:
+            seed = self.seed + self._call_counter
+            self._call_counter += 1
+        _lib.check(_lib.lib().petdiff_generate(
+            self._handle, _ptr(x), _ptr(tac), tseq.ctypes.data_as(C.c_void_p), n, int(bool(flag_var_tilde)),
+            _ptr(zt), int(seed), int(sample_offset), _ptr(out), _ptr(all_xt), B, int(bool(use_graph)),
+            _stream_ptr(self.device)), 'petdiff_generate')
+        if keep_all_xt:
+            return all_xt.cpu().numpy()
+        return out
+
+    generate = ddpm_loop
+
+    def tfunc_ddpm_loop(self, x_T, condition, **kwargs):
+        """diffusion_model.py:718-737: full-T loop, var_tilde, one captured graph."""
+        return self.ddpm_loop(x_T, condition, num_timesteps=None, flag_var_tilde=True, use_graph=True, **kwargs)
+
+    # ---------------------------------------------------------- summaries
+    def posterior_stats(self, x0, tac=None, n_tac=1):
+        """Per (condition, ROI, param) count/mean/M2 (fp64) of samples x0 (main_script.py:433-436)."""
+        h = self._ensure_handle()
+        x = _as_device(x0, self.device, torch.float32)
+        tac_t = None if tac is None else _as_device(tac, self.device, torch.int32)
+        stats = np.zeros((n_tac, x.shape[1], x.shape[2], 3), dtype=np.float64)
+        _lib.check(_lib.lib().petdiff_posterior_stats(h, _ptr(x), _ptr(tac_t), x.shape[0], n_tac,
+                                                      stats.ctypes.data_as(C.c_void_p),
+                                                      _stream_ptr(self.device)), 'petdiff_posterior_stats')
+        return stats
+
+    # ---------------------------------------------------------- timing
+    def set_kernel_timing(self, enable=True):
+        _lib.check(_lib.lib().petdiff_set_timing(self._ensure_handle(), int(enable)))
+
+    def get_kernel_timing(self):
+        ms = (C.c_float * _lib.NUM_LAYERS)()
+        cnt = (C.c_int * _lib.NUM_LAYERS)()
+        _lib.check(_lib.lib().petdiff_get_timing(self._handle, ms, cnt))
+        return {name: (float(ms[i]), int(cnt[i])) for i, name in enumerate(_lib.LAYER_NAMES)}
+
+
+def summarize_stats(stats):
+    """{count, mean, M2} -> per-ROI mean / population std dicts (main_script.py:433-436)."""
+    cnt, mean, m2 = stats[..., 0], stats[..., 1], stats[..., 2]
+    std = np.sqrt(m2 / np.maximum(cnt, 1))
+    return {'mean_DVR': mean[..., 0], 'mean_R1': mean[..., 1], 'std_DVR': std[..., 0], 'std_R1': std[..., 1]}

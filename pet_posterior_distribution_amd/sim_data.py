@@ -1,0 +1,136 @@
+"""Synthetic PET inputs of the reference's shapes (host side, not the hot path).
+
+Restates the data-generation side of the reference so that benchmarks and
+tests have realistic conditions without the Git-LFS test set:
+
+* ``acquisition_time_frames`` -- the 54-frame protocol (sample_sim_data.py:29-85);
+* ``srtm2_tac`` -- SRTM2 forward model (kinetic_model.py:12-57, 142-158), NumPy
+  fp64, used here only to synthesise inputs (the GPU kernel is in petmh);
+* ``noisy_tac`` -- the truncated Poisson-like noise model (sample_sim_data.py:193-215);
+* ``make_condition`` -- condition rows [tac_noisy/dt (48 ROIs) | tac_ref] as in
+  main_script.py:110-113.
+
+The reference's ``prior_stats_nROI48.pik`` is a pickle and is deliberately NOT
+loaded (no unpickling of reference files); ``synthetic_prior`` draws prior
+statistics of the same shapes from a fixed seed instead.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+N_ROI, N_FRAMES = 48, 54
+MK_HALF_T = 109.8   # sample_sim_data.py:95
+
+
+def acquisition_time_frames():
+    """(54, 2) frame [start, end] in minutes (sample_sim_data.py:29-82)."""
+    edges = ([0, 10, 20, 30, 40, 50, 60] + list(range(75, 181, 15)) + list(range(210, 361, 30)) +
+             list(range(420, 841, 60)) + list(range(960, 1801, 120)) + list(range(2100, 7201, 300)))
+    e = np.asarray(edges, dtype=np.float64) / 60.0
+    return np.stack([e[:-1], e[1:]], axis=1)
+
+
+def time_grid():
+    f = acquisition_time_frames()
+    return f[:, 1].copy(), (f[:, 1] - f[:, 0]).copy()     # time_vector, dt (:84-85)
+
+
+def _random_cov_psd(diag, rng, rho=0.5):
+    """helper_func.random_cov_psd (helper_func.py:165-204)."""
+    std = np.sqrt(diag)
+    n = len(diag)
+    A = rng.standard_normal((n, n))
+    Rm = A @ A.T
+    d = np.sqrt(np.diag(Rm))
+    Rm = Rm / d[:, None] / d
+    eig, Q = np.linalg.eigh(Rm)
+    eig = rho * eig + (1 - rho)
+    Rm = Q @ np.diag(eig) @ Q.T
+    return (std[:, None] * Rm) * std
+
+
+def reference_tac(time_vector):
+    """Smooth cerebellum-like reference TAC (arbitrary units, synthetic)."""
+    t = np.asarray(time_vector, dtype=np.float64)
+    return 1.2 * (t / 1.5) * np.exp(1 - t / 1.5) + 0.35 * np.exp(-t / 70.0) * (1 - np.exp(-t / 0.8))
+
+
+def synthetic_prior(seed=2025):
+    """Prior statistics with the shapes of prior_stats_nROI48.pik (synthetic values)."""
+    rng = np.random.default_rng(seed)
+    tv, _ = time_grid()
+    mu_DVR = rng.uniform(0.95, 1.6, N_ROI)
+    mu_R1 = rng.uniform(0.6, 1.0, N_ROI)
+    mu_tac_ref = reference_tac(tv)
+    return dict(mu_DVR=mu_DVR, Cov_DVR=_random_cov_psd((0.08 * mu_DVR) ** 2, rng),
+                mu_R1=mu_R1, Cov_R1=_random_cov_psd((0.06 * mu_R1) ** 2, rng),
+                mu_k2p=np.float64(0.015), mu_tac_ref=mu_tac_ref,
+                Cov_tac_ref=_random_cov_psd((0.03 * mu_tac_ref + 1e-3) ** 2, rng))
+
+
+def interp_matrix(x, xp):
+    """Weights W with  W @ fp == kinetic_model.interp1d_linear_vec(x, xp, fp)  (kinetic_model.py:35-57)."""
+    x = np.asarray(x, dtype=np.float64)
+    xp = np.asarray(xp, dtype=np.float64)
+    dist = np.abs(xp[None, :] - x[:, None])
+    idx = np.searchsorted(xp, x)
+    W = np.zeros_like(dist)
+    r = np.arange(len(idx))
+    W[r, idx] = dist[r, idx - 1]
+    W[r, idx - 1] = dist[r, idx]
+    W /= W.sum(axis=1)[:, None]
+    return W
+
+
+def srtm2_tac(DVR, R1, k2p, tac_ref, time_vector):
+    """SRTM2.create_activity_curve (kinetic_model.py:142-158) -> (54, n_roi) fp64."""
+    DVR = np.asarray(DVR, dtype=np.float64)
+    R1 = np.asarray(R1, dtype=np.float64)
+    tv = np.asarray(time_vector, dtype=np.float64)
+    c_r = np.asarray(tac_ref, dtype=np.float64)
+    k2 = k2p * R1
+    k2a = k2 / DVR
+    c_exp = np.exp(-k2a[None, :] * tv[:, None])                       # (54, n)
+    n = 2 * np.unique(tv).size
+    x_rs = np.linspace(tv.min(), tv.max(), n)
+    dx = x_rs[1] - x_rs[0]
+    y0 = np.interp(x_rs, tv, c_r)
+    y1 = interp_matrix(x_rs, tv) @ c_exp                               # (n, n_roi)
+    conv = np.stack([np.convolve(y0, y1[:, r])[:n] for r in range(y1.shape[1])], axis=1) * dx
+    return R1 * c_r[:, None] + (k2 - R1 * k2a) * (interp_matrix(tv, x_rs) @ conv)
+
+
+def noisy_tac(tac, dt, time_vector, sigma_roi, rng):
+    """Noise model of sample_sim_data.py:193-215; tac (n_roi, 54) concentration."""
+    from scipy.stats import truncnorm
+    lam = np.log(2) / MK_HALF_T
+    sigma_noise = sigma_roi[:, None] / np.sqrt(dt[None, :] * np.exp(-lam * time_vector))
+    x = np.maximum(tac, 0.0)
+    s = np.sqrt(x)
+    low = (-s) / sigma_noise
+    e = truncnorm.rvs(low, np.inf, loc=0.0, scale=sigma_noise, random_state=rng)
+    return x + s * e, sigma_noise
+
+
+def make_condition(seed=0, prior=None, mean_sigma_noise=0.1, return_truth=False):
+    """One synthetic test TAC -> condition (49, 54) float32 (main_script.py:110-113)."""
+    prior = prior or synthetic_prior()
+    rng = np.random.default_rng(seed)
+    tv, dt = time_grid()
+    while True:
+        DVR = rng.multivariate_normal(prior['mu_DVR'], prior['Cov_DVR'])
+        R1 = rng.multivariate_normal(prior['mu_R1'], prior['Cov_R1'])
+        ref = rng.multivariate_normal(prior['mu_tac_ref'], prior['Cov_tac_ref'])
+        if (DVR > 0).all() and (R1 > 0).all() and (ref > 0).all():
+            tac = srtm2_tac(DVR, R1, prior['mu_k2p'], ref, tv).T          # (48, 54)
+            if (tac >= 0).all():
+                break
+    from scipy.stats import truncnorm
+    sigma_roi = truncnorm.rvs(-1 / 0.3, np.inf, loc=mean_sigma_noise, scale=0.3 * mean_sigma_noise,
+                              size=N_ROI, random_state=rng)
+    tac_noisy, sigma_noise = noisy_tac(tac, dt, tv, sigma_roi, rng)
+    cond = np.concatenate([tac_noisy, ref[None, :]], axis=0).astype(np.float32)
+    if return_truth:
+        return cond, dict(DVR=DVR, R1=R1, k2p=prior['mu_k2p'], tac_ref=ref, tac=tac,
+                          sigma_noise=sigma_noise, time_vector=tv, dt=dt)
+    return cond

@@ -1,0 +1,217 @@
+"""GPU parity tests: libpetdiff (HIP, gfx950) vs the CPU oracle (oracle/iddpm_ref.py).
+
+Tolerances (written per test):
+* exact-f32 MFMA network: max|gpu - oracle_fp64| <= 1e-4 * max|oracle| (north_star: 1e-4 rtol);
+* bf16 network (fp32 accumulate): <= 3e-2 * max|oracle| on one forward;
+* p_sample / loop with identical injected noise: posterior mean / SD within 1e-4 rtol.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import iddpm_ref as R
+from tests.helpers import shipped_net_args, shipped_diff_args, synthetic_condition
+
+pytestmark = pytest.mark.gpu
+
+S = R.schedule_tables(R.get_beta_schedule('cosine', 1000))
+
+
+def make_model(dtype='float32', seed=11, bias_scale=0.05, learn_variance='learn_ranged', parameterization='eps',
+               final_scale=1.0):
+    from pet_posterior_distribution_amd import ImprovedDDPM, UnetConditional, denoiser_init
+    args = shipped_net_args()
+    args['learn_variance'] = learn_variance
+    net = UnetConditional(**args)
+    net.build((None, 48, 2))
+    net.weights = denoiser_init(net.spec(), seed=seed, bias_scale=bias_scale, perturb=0.1 * final_scale)
+    return ImprovedDDPM(network=net, dtype=dtype, parameterization=parameterization, **shipped_diff_args())
+
+
+def rel(a, b):
+    a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+    return float(np.abs(a.astype(np.float64) - b).max() / (np.abs(b).max() + 1e-30))
+
+
+@pytest.fixture(scope='module')
+def conds():
+    return np.stack([synthetic_condition(0), synthetic_condition(1)])
+
+
+@pytest.fixture(scope='module')
+def m32():
+    return make_model('float32')
+
+
+@pytest.fixture(scope='module')
+def m16():
+    return make_model('bfloat16')
+
+
+def test_unet_forward_f32(m32, conds):
+    rng = np.random.default_rng(1)
+    B = 8
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    t = np.array([999, 998, 500, 250, 17, 2, 1, 0], dtype=np.int32)
+    cond = conds[np.array([0, 1, 1, 0, 0, 1, 0, 1])]
+    out = m32.call({'x': x, 'time': t, 'condition': cond})
+    ref = R.unet_forward(m32.network.weights, x, t, cond, dt=np.float64)
+    assert out.shape == (B, 48, 4)
+    assert rel(out, ref) < 1e-4
+
+
+def test_unet_forward_bf16(m16, conds):
+    rng = np.random.default_rng(2)
+    B = 8
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    t = np.array([999, 700, 500, 250, 17, 2, 1, 0], dtype=np.int32)
+    cond = np.repeat(conds[:1], B, 0)
+    out = m16.call({'x': x, 'time': t, 'condition': cond})
+    ref = R.unet_forward(m16.network.weights, x, t, cond, dt=np.float64)
+    assert rel(out, ref) < 3e-2
+
+
+@pytest.mark.parametrize('B', [1, 5, 37])
+def test_ragged_batches_f32(m32, conds, B):
+    """Batches that do not fill a 192-row tile (4 samples at L=48, 32 at L=6)."""
+    rng = np.random.default_rng(B)
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    t = rng.integers(0, 1000, B).astype(np.int32)
+    cond = np.repeat(conds[:1], B, 0)
+    out = m32.call({'x': x, 'time': t, 'condition': cond})
+    ref = R.unet_forward(m32.network.weights, x, t, cond, dt=np.float64)
+    assert rel(out, ref) < 1e-4
+
+
+def test_p_sample_injected_noise(m32, conds):
+    rng = np.random.default_rng(3)
+    B = 6
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    t = np.array([999, 600, 100, 2, 1, 0], dtype=np.int32)
+    z = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    cond = np.repeat(conds[1:], B, 0)
+    mean, var, var_t = m32.ddpm(x, t, cond, z=z)
+    rm, rv, rvt = R.ddpm(m32.network.weights, S, x, t, cond, z, dt=np.float64)
+    assert rel(mean, rm) < 1e-4
+    assert rel(var, rv) < 1e-4
+    assert rel(var_t, rvt) < 1e-4
+    assert float(var[-1].abs().max()) == 0.0          # t == 0: no noise (diffusion_model.py:658)
+
+
+@pytest.mark.parametrize('lv,param', [('', 'eps'), ('learn', 'eps'), ('learn_ranged', 'v'),
+                                      ('learn_ranged', 'x0'), ('learn_ranged', 'x_prev')])
+def test_p_sample_variants(conds, lv, param):
+    m = make_model('float32', seed=5, learn_variance=lv, parameterization=param, final_scale=0.2)
+    rng = np.random.default_rng(4)
+    B = 4
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    t = np.array([999, 400, 3, 0], dtype=np.int32)
+    z = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    cond = np.repeat(conds[:1], B, 0)
+    mean, var, var_t = m.ddpm(x, t, cond, z=z)
+    rm, rv, rvt = R.ddpm(m.network.weights, S, x, t, cond, z, learn_variance=lv, parameterization=param,
+                         dt=np.float64)
+    assert rel(mean, rm) < 1e-4
+    assert rel(var, rv) < 1e-4
+    assert rel(var_t, rvt) < 1e-4
+    m.close()
+
+
+def test_philox_noise_matches_oracle(m32, conds):
+    rng = np.random.default_rng(5)
+    B = 4
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    t = np.full(B, 700, dtype=np.int32)
+    cond = np.repeat(conds[:1], B, 0)
+    seed, off, step = 987654321123, 1000, 17
+    mean, var, _ = m32.ddpm(x, t, cond, seed=seed, sample_offset=off, rng_step=step)
+    z = R.philox_normal_pairs(seed, off + np.arange(B), step)
+    rm, rv, _ = R.ddpm(m32.network.weights, S, x, t, cond, z, dt=np.float64)
+    assert rel(var, rv) < 1e-4
+
+
+@pytest.mark.parametrize('sub', ['linear', 'quadratic'])
+def test_loop_injected_noise_f32(m32, conds, sub):
+    rng = np.random.default_rng(6)
+    B = 8
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    idx = R.loop_indices(1000, 20, sub)
+    z = rng.standard_normal((len(idx), B, 48, 2)).astype(np.float32)
+    out = m32.ddpm_loop(x, conds[:1], num_timesteps=20, sub_sequence_type=sub, z=z)
+    ref = R.ddpm_loop(m32.network.weights, S, x, conds[:1], z, idx, dt=np.float64)
+    assert rel(out, ref) < 1e-4
+    o = out.cpu().numpy().astype(np.float64)
+    for f in (np.mean, np.std):
+        assert rel(f(o, axis=0), f(ref, axis=0)) < 1e-4
+
+
+def test_loop_full_1000_steps_f32(m32, conds):
+    """Full T=1000 reverse process (the metric's path) at small B vs the oracle."""
+    rng = np.random.default_rng(7)
+    B = 2
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    idx = R.loop_indices(1000)
+    z = rng.standard_normal((len(idx), B, 48, 2)).astype(np.float32)
+    out = m32.ddpm_loop(x, conds[:1], z=z)
+    ref = R.ddpm_loop(m32.network.weights, S, x, conds[:1], z, idx, dt=np.float64)
+    assert rel(out, ref) < 1e-4
+
+
+def test_keep_all_xt(m32, conds):
+    rng = np.random.default_rng(8)
+    x = rng.standard_normal((3, 48, 2)).astype(np.float32)
+    allx = m32.ddpm_loop(x, conds[:1], num_timesteps=5, keep_all_xt=True, seed=3)
+    last = m32.ddpm_loop(x, conds[:1], num_timesteps=5, seed=3)
+    assert allx.shape == (5, 3, 48, 2)
+    np.testing.assert_array_equal(allx[-1], last.cpu().numpy())
+
+
+def test_graph_equals_eager_and_shard_invariance(m16, conds):
+    """hipGraph replay == eager launch, and splitting a batch (sample_offset) is bitwise neutral."""
+    rng = np.random.default_rng(9)
+    B = 64
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    a = m16.ddpm_loop(x, conds[:1], num_timesteps=50, seed=42, use_graph=True)
+    b = m16.ddpm_loop(x, conds[:1], num_timesteps=50, seed=42, use_graph=False)
+    c1 = m16.ddpm_loop(x[:24], conds[:1], num_timesteps=50, seed=42, sample_offset=0)
+    c2 = m16.ddpm_loop(x[24:], conds[:1], num_timesteps=50, seed=42, sample_offset=24)
+    torch.testing.assert_close(a, b, rtol=0, atol=0)
+    torch.testing.assert_close(a, torch.cat([c1, c2]), rtol=0, atol=0)
+
+
+def test_bf16_loop_statistics_vs_f32(m16, m32, conds):
+    """bf16 network vs exact-f32 network on the same noise: posterior moments agree statistically."""
+    rng = np.random.default_rng(10)
+    B = 256
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    a = m16.ddpm_loop(x, conds[:1], num_timesteps=100, seed=5).cpu().numpy()
+    b = m32.ddpm_loop(x, conds[:1], num_timesteps=100, seed=5).cpu().numpy()
+    assert np.isfinite(a).all()
+    scale = np.abs(b).mean()
+    assert np.abs(a.mean(0) - b.mean(0)).max() < 0.1 * scale
+
+
+def test_posterior_stats(m32):
+    rng = np.random.default_rng(11)
+    B = 1000
+    x0 = rng.standard_normal((B, 48, 2)).astype(np.float32) * 3 + 1
+    tac = (np.arange(B) % 3).astype(np.int32)
+    st = m32.posterior_stats(x0, tac, n_tac=3)
+    for k in range(3):
+        xs = x0[tac == k].astype(np.float64)
+        np.testing.assert_allclose(st[k, :, :, 0], xs.shape[0])
+        np.testing.assert_allclose(st[k, :, :, 1], xs.mean(0), rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(np.sqrt(st[k, :, :, 2] / xs.shape[0]), xs.std(0), rtol=1e-10)
+
+
+def test_full_size_config_properties(m16, conds):
+    """BASELINE config 2 at full size (B=1024, 1000 steps, bf16): finite, deterministic, chunk-invariant."""
+    rng = np.random.default_rng(12)
+    B = 1024
+    x = torch.as_tensor(rng.standard_normal((B, 48, 2)).astype(np.float32), device='cuda')
+    a = m16.ddpm_loop(x, conds[:1], seed=77)
+    b = m16.ddpm_loop(x, conds[:1], seed=77)
+    assert torch.isfinite(a).all()
+    torch.testing.assert_close(a, b, rtol=0, atol=0)
+    half = m16.ddpm_loop(x[512:], conds[:1], seed=77, sample_offset=512)
+    torch.testing.assert_close(a[512:], half, rtol=0, atol=0)
