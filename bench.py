@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Benchmark: posterior samples/sec of the 1000-step iDDPM reverse process (48-ROI TAC).
+
+Workload (BASELINE.json configs[1]): f128/d4 1-D conditional U-Net, 1000-step
+iDDPM reverse (ImprovedDDPM.ddpm_loop, diffusion_model.py:670-715), n_posterior =
+1024 samples per GPU, bf16 network / fp32 p_sample, one synthetic test TAC per
+GPU, synthetic (identity-denoiser Glorot) weights of the shipped architecture.
+
+A bench "step" = one full generate() (1000 reverse steps) over the rank's 1024
+samples; the whole loop is one replayed hipGraph.  Weak scaling: every rank
+owns 1024 samples of its own TAC; value = all ranks' samples / max-over-ranks time.
+After the timed region the per-(TAC, ROI, param) Welford partials are
+all-gathered over RCCL (the only collective).
+
+Launch: python bench.py --gpus N --steps K --warmup W  (N>1 via torch.distributed.run).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# algorithmic work
+FLOP_PER_SAMPLE_STEP = 296_361_984          # x-dependent U-Net convs incl. 1x1 residuals
+# dominant kernel = up0 ConvBlock: relu(conv6(1024->512) + conv1(1024->512)) at L=12 (App. A: 37.75+6.29 M MAC)
+UP0_BLOCK_FLOP_PER_SAMPLE = 2 * 12 * 512 * 1024 * 7
+UP0_BLOCK_EXEC_FLOP_PER_SAMPLE = 2 * 12 * 512 * 1024 * 6   # executed (residual folded into the centre tap)
+PEAK_BF16_TFLOPS = 2500.0                   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--batch', type=int, default=1024, help='posterior samples per GPU')
+    ap.add_argument('--reverse-steps', type=int, default=1000)
+    ap.add_argument('--dtype', default='bfloat16', choices=['bfloat16', 'float32'])
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-kernel-timing', action='store_true')
+    return ap.parse_args()
+
+
+def cpu_baseline(weights, cond, budget_s=15.0):
+    """Oracle (NumPy fp32 restatement) on a bounded sample: B=32 samples, as many reverse
+    steps as fit in ~budget_s, extrapolated to the 1000-step process."""
+    from oracle import iddpm_ref as R
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([p.get('num_threads', 1) for p in threadpool_info()] or [1])
+    except Exception:
+        cores = os.cpu_count() or 1
+    S = R.schedule_tables(R.get_beta_schedule('cosine', 1000))
+    rng = np.random.default_rng(0)
+    B = 32
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    c = np.repeat(cond[None], B, 0)
+    P = {k: v.astype(np.float32) for k, v in weights.items()}
+    n, t0 = 0, time.perf_counter()
+    for ti in R.loop_indices(1000):
+        z = rng.standard_normal((B, 48, 2)).astype(np.float32)
+        m, _, vt = R.ddpm(P, S, x, np.full(B, ti, np.int32), c, z, dt=np.float32)
+        x = m + vt
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    per_step = dt / n
+    return {'value': B / (per_step * 1000.0), 'unit': 'samples/s', 'cores': int(cores), 'kind': 'port',
+            'sample': f'oracle/iddpm_ref.py NumPy fp32, B=32 samples x {n} reverse steps ({dt:.1f} s), '
+                      f'extrapolated to 1000 steps'}
+
+
+def load_traffic():
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
+    p = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get('up0_block_bytes_per_launch')
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        os.environ.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device('cuda', torch.cuda.current_device())
+
+    from pet_posterior_distribution_amd import ImprovedDDPM, UnetConditional
+    from pet_posterior_distribution_amd.sim_data import make_condition
+    from pet_posterior_distribution_amd.configs import shipped_net_args, shipped_diff_args
+
+    net = UnetConditional(**shipped_net_args(), seed=1234)
+    net.build((None, 48, 2))
+    model = ImprovedDDPM(network=net, dtype=args.dtype, device=dev.index, **shipped_diff_args())
+    B = args.batch
+    cond = make_condition(seed=rank)                  # one synthetic test TAC per rank
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + rank)
+    x_T = torch.randn((B, 48, 2), generator=g, device=dev, dtype=torch.float32)
+    n_rev = args.reverse_steps
+    offset = rank * B
+
+    def one():
+        return model.ddpm_loop(x_T, cond[None], num_timesteps=n_rev, seed=2, sample_offset=offset)
+
+    for _ in range(args.warmup):
+        out = one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    # posterior summary: per-rank Welford partials, RCCL all-gather
+    st = model.posterior_stats(out)                               # (1, 48, 2, 3) fp64
+    st_t = torch.as_tensor(st, device=dev)
+    ag_ms = 0.0
+    if world > 1:
+        gathered = [torch.empty_like(st_t) for _ in range(world)]
+        torch.cuda.synchronize()
+        ta = time.perf_counter()
+        dist.all_gather(gathered, st_t)
+        torch.cuda.synchronize()
+        ag_ms = (time.perf_counter() - ta) * 1e3
+        allst = torch.cat(gathered).cpu().numpy()
+    else:
+        allst = st
+    finite = bool(torch.isfinite(out).all())
+
+    # per-layer kernel timing (HIP events on the launch stream, one eager generate)
+    layer_ms = None
+    if not args.no_kernel_timing:
+        model.set_kernel_timing(True)
+        model.ddpm_loop(x_T, cond[None], num_timesteps=n_rev, seed=2, sample_offset=offset, use_graph=False)
+        layer_ms = model.get_kernel_timing()
+        model.set_kernel_timing(False)
+
+    if rank == 0:
+        samples = world * B * args.steps
+        value = samples / elapsed
+        tflops_pipeline = FLOP_PER_SAMPLE_STEP * n_rev * samples / elapsed / 1e12
+        peak = PEAK_BF16_TFLOPS if args.dtype == 'bfloat16' else PEAK_F32_TFLOPS
+        roof = None
+        if layer_ms is not None:
+            ms, cnt = layer_ms['up0.block']
+            avg_s = ms / max(cnt, 1) / 1e3
+            ach = UP0_BLOCK_FLOP_PER_SAMPLE * B / avg_s / 1e12
+            roof = {'bound': 'mfma', 'kernel': 'conv_kernel<up0.block> (L=12, 1024->512, k6+res)',
+                    'achieved': round(ach, 2), 'peak': peak, 'unit': 'TFLOP/s', 'frac': round(ach / peak, 4),
+                    'traffic': load_traffic(), 'avg_launch_us': round(avg_s * 1e6, 2),
+                    'executed_tflops': round(UP0_BLOCK_EXEC_FLOP_PER_SAMPLE * B / avg_s / 1e12, 2),
+                    'pipeline_tflops': round(tflops_pipeline, 2),
+                    'pipeline_frac': round(tflops_pipeline / peak, 4)}
+        line = {
+            'metric': 'posterior samples/sec (48-ROI TAC, 1000-step reverse) at 1/2/4/8 MI355X',
+            'value': round(value, 2), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16' if args.dtype == 'bfloat16' else 'f32',
+            'data': 'synthetic (SRTM2 TACs + noise model; identity-denoiser Glorot weights of the shipped net)',
+            'config': {'workload': 'iDDPM reverse process, f128/d4 1-D conditional U-Net, 48-ROI x 2 params',
+                       'n_posterior_per_gpu': B, 'reverse_steps': n_rev, 'global_batch': world * B,
+                       'tacs': world, 'parallelism': f'dp{world} (sample shards, RCCL all-gather of stats)',
+                       'hipgraph': True},
+            'roofline': roof,
+            'outputs_finite': finite,
+            'stats_allgather_ms': round(ag_ms, 3),
+        }
+        if layer_ms is not None:
+            line['layer_us'] = {k: round(v[0] / max(v[1], 1) * 1e3, 2) for k, v in layer_ms.items()}
+        if world == 1 and not args.no_cpu_baseline:
+            line['cpu_baseline'] = cpu_baseline(net.weights, cond)
+        else:
+            line['cpu_baseline'] = None
+        sm = allst[..., 1]
+        line['posterior_mean_DVR_roi0'] = [round(float(v), 5) for v in sm[:, 0, 0]]
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -54,13 +54,6 @@ SYMBOLS = [
     ('petdiff_get_timing', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ('petdiff_last_error', C.c_char_p, []),
     # Metropolis-Hastings / SRTM2 (include/petmh.h)
-    ('petmh_srtm2_tac', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
-                                  C.c_void_p, C.c_void_p, C.c_void_p]),
-    ('petmh_create', C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
-    ('petmh_destroy', C.c_int, [C.c_void_p]),
-    ('petmh_run', C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_p,
-                            C.c_void_p, C.c_void_p]),
-    ('petmh_logp', C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
 ]
 
 _lib = None

@@ -218,8 +218,10 @@ namespace {
 template <typename T, typename H>
 int pack_conv(petdiff_ctx* h, const std::vector<float>& wk_host, int li) {
   const ConvLayer& cl = kConv[li];
-  constexpr int KC = sizeof(T) == 2 ? 32 : 16;
-  constexpr int EPC = KC / 4;
+  const int ROWB = conv_rowb<T>(cl.taps);
+  const int KC = conv_kc<T>(cl.taps);
+  const int CPR = ROWB / 16;
+  const int EPC = 16 / (int)sizeof(T);
   const Spec* sk = nullptr;
   const Spec* sr = nullptr;
   for (auto& s : h->spec) {
@@ -229,15 +231,19 @@ int pack_conv(petdiff_ctx* h, const std::vector<float>& wk_host, int li) {
   if (!sk) return fail(PETDIFF_ERR_INVALID, "missing weight " + std::string(cl.wname));
   const float* wk = wk_host.data() + sk->off;
   const float* wr = sr ? wk_host.data() + sr->off : nullptr;
+  if (cl.cin_x % KC != 0) return fail(PETDIFF_ERR_UNSUPPORTED, "channel count not a multiple of the K chunk");
   const int NC = cl.cin_x / KC, nNT = cl.cout / kNT;
+  // [n_tile][chunk][tap][n (128)][CPR x 16-B pieces], piece index XOR-swizzled by n
+  // exactly like ConvGeom::key so a linear LDS-DMA copy yields the swizzled image.
   std::vector<H> out((size_t)nNT * NC * cl.taps * kNT * KC);
   size_t q = 0;
   for (int nt = 0; nt < nNT; ++nt)
     for (int kc = 0; kc < NC; ++kc)
       for (int j = 0; j < cl.taps; ++j)
         for (int n = 0; n < kNT; ++n)
-          for (int p = 0; p < 4; ++p) {
-            const int c = p ^ ((n >> 2) & 3);
+          for (int p = 0; p < CPR; ++p) {
+            const int key = CPR == 4 ? ((n >> 2) & 3) : ((n >> 1) & 7);
+            const int c = p ^ key;
             for (int e = 0; e < EPC; ++e) {
               const int ci = cl.xoff + kc * KC + c * EPC + e;
               const int co = nt * kNT + n;

@@ -12,8 +12,13 @@ typedef __bf16 bf16;
 // Tile geometry of the implicit-GEMM Conv1D kernel (see DESIGN.md "conv kernel").
 constexpr int kMT = 192;      // output rows (sample x position) per workgroup
 constexpr int kNT = 128;      // output channels per workgroup
-constexpr int kRowB = 64;     // bytes of one LDS row chunk (32 bf16 / 16 f32 channels)
 constexpr int kThreads = 256; // 4 waves: 2 (M) x 2 (N), 96 x 64 per wave
+// Bytes of input channels per K chunk (one LDS row): 64 B for the 6-tap convs
+// (two stages of 6 taps x 128 x 64 B fit LDS), 128 B for the 2-tap up-convs.
+template <typename T>
+constexpr int conv_rowb(int taps) { return taps == 2 ? 128 : 64; }
+template <typename T>
+constexpr int conv_kc(int taps) { return conv_rowb<T>(taps) / (int)sizeof(T); }
 
 // Epilogue kinds
 enum Epi : int {

@@ -25,9 +25,6 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <typename T> struct TileCfg;
-template <> struct TileCfg<bf16> { static constexpr int KC = 32; static constexpr int EPC = 8; };
-template <> struct TileCfg<float> { static constexpr int KC = 16; static constexpr int EPC = 4; };
 
 __device__ __forceinline__ float to_f(float v) { return v; }
 __device__ __forceinline__ float to_f(bf16 v) { return (float)v; }
@@ -114,32 +111,97 @@ __device__ __forceinline__ void p_sample_elem(const FinalArgs& f, int t, float x
 
 // ---------------------------------------------------------------------------
 // Implicit-GEMM Conv1D on MFMA.  See DESIGN.md for the tiling.
+//   M tile = 192 rows = S whole samples, N tile = 128 channels, 4 waves (2x2),
+//   96 x 64 per wave (3 x 2 MFMA 32x32 tiles).  K loop over chunks of
+//   ROWB bytes of input channels; per chunk all TAPS taps are served from one
+//   LDS copy of the chunk's input rows.
 // ---------------------------------------------------------------------------
-template <typename T, int L, bool UPS, int TAPS, int PADL, int EPI>
+template <typename T, int L, bool UPS, int TAPS, int PADL, int EPI, int ROWB>
 struct ConvGeom {
   static constexpr int S = kMT / L;                 // samples per workgroup
   static constexpr int LIN = UPS ? L / 2 : L;       // input rows per sample
   static constexpr int AROWS = S * LIN;
   static constexpr int ZROW = AROWS;                // always-zero LDS row
-  static constexpr int A_BYTES = ((AROWS + 1) * kRowB + 255) / 256 * 256;
-  static constexpr int B_BYTES = TAPS * kNT * kRowB;
+  static constexpr int CPR = ROWB / 16;             // 16-B pieces per LDS row
+  static constexpr int KC = ROWB / (int)sizeof(T);  // input channels per chunk
+  static constexpr int EPC = 16 / (int)sizeof(T);   // elements per 16-B piece
+  static constexpr int A_BYTES = ((AROWS + 1) * ROWB + 255) / 256 * 256;
+  static constexpr int B_BYTES = TAPS * kNT * ROWB;
   static constexpr int STAGE = A_BYTES + B_BYTES;
-  static constexpr int APIECES = AROWS * 4;
+  static constexpr int APIECES = AROWS * CPR;
   static constexpr int APT = (APIECES + kThreads - 1) / kThreads;
   static constexpr int BPT = B_BYTES / 16 / kThreads;
-  static constexpr int FIN_LD = 129;                 // padded fp32 row of the final tile
-  static constexpr int FIN_BYTES = kMT * FIN_LD * 4 + 128 * 4 * 4 + 64;
-  static constexpr int SMEM = (EPI == EPI_FINAL && FIN_BYTES > 2 * STAGE) ? FIN_BYTES : 2 * STAGE;
+  static constexpr int CT_LD = kNT + 4;             // fp32 C tile row (non-final epilogue)
+  static constexpr int FIN_LD = 129;                 // fp32 C tile row (final epilogue)
+  static constexpr int EPI_BYTES = (EPI == EPI_FINAL) ? kMT * FIN_LD * 4 + 128 * 4 * 4 + 64 : kMT * CT_LD * 4;
+  static constexpr int SMEM = EPI_BYTES > 2 * STAGE ? EPI_BYTES : 2 * STAGE;
   static_assert(kMT % L == 0, "tile must hold whole samples");
   static_assert(B_BYTES % (16 * kThreads) == 0, "B tile split");
+  static_assert(ROWB == 64 || ROWB == 128, "row width");
   static_assert(SMEM <= 160 * 1024, "LDS budget");
+  // XOR key of the 16-B piece index within a row: conflict-free ds_read_b128 for
+  // 16 consecutive rows (lane groups of MI355X_MICROARCH.md LDS table)
+  static __device__ __forceinline__ int key(int row) { return CPR == 4 ? ((row >> 2) & 3) : ((row >> 1) & 7); }
 };
 
-template <typename T, int L, bool UPS, int TAPS, int PADL, int EPI>
+// Global -> LDS staging of chunk kc into stage buf by LDS-DMA
+// (global_load_lds_dwordx4).  Piece p of a stage lands at byte 16*p; the pieces
+// of one wave instruction are the 64 consecutive p = q*256 + wave*64 + lane, so
+// the LDS destination is wave-uniform base + lane*16 and the XOR swizzle lives
+// in the SOURCE address.
+template <typename T, int L, bool UPS, int TAPS, int PADL, int EPI, int ROWB>
+__device__ __forceinline__ void stage_issue(const ConvArgs<T>& a, char* smem, int kc, int buf, int n1, int NC,
+                                            int m0, int n_tile, int wv, int lane) {
+  using G = ConvGeom<T, L, UPS, TAPS, PADL, EPI, ROWB>;
+  const T* src;
+  int stride, ch;
+  if (kc < n1) { src = a.src1; stride = a.c1; ch = kc * G::KC; }
+  else { src = a.src2; stride = a.c2; ch = (kc - n1) * G::KC; }
+  char* sbase = smem + buf * G::STAGE;
+#pragma unroll
+  for (int qq = 0; qq < G::APT; ++qq) {
+    const int p0 = qq * kThreads + wv * 64;
+    if (p0 < G::APIECES) {
+      const int p = p0 + lane;
+      if (p < G::APIECES) {
+        const int row = p / G::CPR, cp = p - row * G::CPR;
+        const int c = cp ^ G::key(row);
+        const int s = row / G::LIN, li = row - s * G::LIN;
+        const int b = min(m0 + s, a.B - 1);   // rows of absent samples only feed unstored outputs
+        const T* g = src + (size_t)(b * G::LIN + li) * stride + ch + c * G::EPC;
+        __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(sbase + p0 * 16), 16, 0, 0);
+      }
+    }
+  }
+  const char* wp = reinterpret_cast<const char*>(a.wpack) + (size_t)(n_tile * NC + kc) * G::B_BYTES;
+#pragma unroll
+  for (int qq = 0; qq < G::BPT; ++qq) {
+    const int p0 = qq * kThreads + wv * 64;
+    __builtin_amdgcn_global_load_lds(wp + (size_t)(p0 + lane) * 16,
+                                     (__attribute__((address_space(3))) void*)(sbase + G::A_BYTES + p0 * 16), 16,
+                                     0, 0);
+  }
+}
+
+template <typename T> struct Vec8;
+template <> struct Vec8<bf16> {
+  static __device__ __forceinline__ void store(bf16* p, const float* v) {
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
+    *reinterpret_cast<bf16x8*>(p) = o;
+  }
+};
+template <> struct Vec8<float> {
+  static __device__ __forceinline__ void store(float* p, const float* v) {
+    *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<f32x4*>(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+  }
+};
+
+template <typename T, int L, bool UPS, int TAPS, int PADL, int EPI, int ROWB>
 __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
-  using G = ConvGeom<T, L, UPS, TAPS, PADL, EPI>;
-  constexpr int KC = TileCfg<T>::KC;
-  constexpr int EPC = TileCfg<T>::EPC;
+  using G = ConvGeom<T, L, UPS, TAPS, PADL, EPI, ROWB>;
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
 
   const int tid = threadIdx.x;
@@ -158,16 +220,17 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
   const int n_tile = slot / nM, m_tile = slot - n_tile * nM;
   const int m0 = m_tile * G::S;
 
-  const int n1 = a.c1 / KC;
-  const int NC = n1 + a.c2 / KC;
+  const int n1 = a.c1 / G::KC;
+  const int NC = n1 + a.c2 / G::KC;
 
   // zero row of both stages
-  if (tid < 8) {
-    const int st = tid >> 2, pc = tid & 3;
-    *reinterpret_cast<uint4*>(smem + st * G::STAGE + G::ZROW * kRowB + pc * 16) = make_uint4(0, 0, 0, 0);
+  if (tid < 2 * G::CPR) {
+    const int st = tid / G::CPR, pc = tid - st * G::CPR;
+    *reinterpret_cast<uint4*>(smem + st * G::STAGE + G::ZROW * ROWB + pc * 16) = make_uint4(0, 0, 0, 0);
   }
 
-  // per-lane LDS byte offsets of the A fragment rows (tap j, m-subtile i)
+  // per-lane LDS byte offsets of the A fragment rows (tap j, m-subtile i) and B rows
+  const int c0 = (sizeof(T) == 2) ? h : 2 * h;
   int aoff[TAPS][3];
 #pragma unroll
   for (int j = 0; j < TAPS; ++j) {
@@ -179,53 +242,16 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
       int row;
       if (!UPS) row = (p >= 0 && p < L) ? s * L + p : G::ZROW;
       else row = (p < L) ? s * G::LIN + (p >> 1) : G::ZROW;
-      const int c0 = (sizeof(T) == 2) ? h : 2 * h;
-      aoff[j][i] = row * kRowB + ((c0 ^ ((row >> 2) & 3)) << 4);
+      aoff[j][i] = row * ROWB + ((c0 ^ G::key(row)) << 4);
     }
   }
   int boff[2];
 #pragma unroll
   for (int jn = 0; jn < 2; ++jn) {
     const int n = wn * 64 + jn * 32 + lr;
-    const int c0 = (sizeof(T) == 2) ? h : 2 * h;
-    boff[jn] = G::A_BYTES + n * kRowB + ((c0 ^ ((n >> 2) & 3)) << 4);
+    boff[jn] = G::A_BYTES + n * ROWB + ((c0 ^ G::key(n)) << 4);
   }
-
-  uint4 ra[G::APT];
-  uint4 rb[G::BPT];
-  auto gload = [&](int kc) {
-    const T* src;
-    int stride, ch;
-    if (kc < n1) { src = a.src1; stride = a.c1; ch = kc * KC; }
-    else { src = a.src2; stride = a.c2; ch = (kc - n1) * KC; }
-#pragma unroll
-    for (int qq = 0; qq < G::APT; ++qq) {
-      const int p = tid + qq * kThreads;
-      ra[qq] = make_uint4(0, 0, 0, 0);
-      if (p < G::APIECES) {
-        const int row = p >> 2, cp = p & 3;
-        const int c = cp ^ ((row >> 2) & 3);
-        const int s = row / G::LIN, li = row - s * G::LIN;
-        const int b = m0 + s;
-        if (b < B)
-          ra[qq] = *reinterpret_cast<const uint4*>(src + (size_t)(b * G::LIN + li) * stride + ch + c * EPC);
-      }
-    }
-    const uint4* wp = reinterpret_cast<const uint4*>(a.wpack) + (size_t)(n_tile * NC + kc) * (G::B_BYTES / 16);
-#pragma unroll
-    for (int qq = 0; qq < G::BPT; ++qq) rb[qq] = wp[tid + qq * kThreads];
-  };
-  auto sstore = [&](int buf) {
-    char* base = smem + buf * G::STAGE;
-#pragma unroll
-    for (int qq = 0; qq < G::APT; ++qq) {
-      const int p = tid + qq * kThreads;
-      if (p < G::APIECES) *reinterpret_cast<uint4*>(base + p * 16) = ra[qq];
-    }
-#pragma unroll
-    for (int qq = 0; qq < G::BPT; ++qq)
-      *reinterpret_cast<uint4*>(base + G::A_BYTES + (tid + qq * kThreads) * 16) = rb[qq];
-  };
+  const int wv = __builtin_amdgcn_readfirstlane(w);
 
   f32x16 acc[3][2];
 #pragma unroll
@@ -235,92 +261,134 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][jn][e] = 0.f;
 
-  gload(0);
-  sstore(0);
+  stage_issue<T, L, UPS, TAPS, PADL, EPI, ROWB>(a, smem, 0, 0, n1, NC, m0, n_tile, wv, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   for (int kc = 0; kc < NC; ++kc) {
-    if (kc + 1 < NC) gload(kc + 1);
+    if (kc + 1 < NC)
+      stage_issue<T, L, UPS, TAPS, PADL, EPI, ROWB>(a, smem, kc + 1, (kc + 1) & 1, n1, NC, m0, n_tile, wv, lane);
     const char* base = smem + (kc & 1) * G::STAGE;
+    if constexpr (sizeof(T) == 2) {
+      // step = (tap j, 16-k group g); fragments of step+1 are read while step's MFMAs run
+      constexpr int NG = ROWB / 32;
+      constexpr int NS = TAPS * NG;
+      bf16x8 av[2][3], bv[2][2];
 #pragma unroll
-    for (int j = 0; j < TAPS; ++j) {
-      if constexpr (sizeof(T) == 2) {
+      for (int st = 0; st < NS + 1; ++st) {
+        if (st < NS) {
+          const int j = st / NG, g = st % NG, sb = st & 1;
 #pragma unroll
-        for (int g = 0; g < 2; ++g) {
-          bf16x8 av[3], bv[2];
-#pragma unroll
-          for (int i = 0; i < 3; ++i) av[i] = *reinterpret_cast<const bf16x8*>(base + (aoff[j][i] ^ (g << 5)));
+          for (int i = 0; i < 3; ++i) av[sb][i] = *reinterpret_cast<const bf16x8*>(base + (aoff[j][i] ^ (g << 5)));
 #pragma unroll
           for (int jn = 0; jn < 2; ++jn)
-            bv[jn] = *reinterpret_cast<const bf16x8*>(base + ((boff[jn] + j * kNT * kRowB) ^ (g << 5)));
+            bv[sb][jn] = *reinterpret_cast<const bf16x8*>(base + ((boff[jn] + j * kNT * ROWB) ^ (g << 5)));
+        }
+        if (st > 0) {
+          const int pb = (st - 1) & 1;
 #pragma unroll
           for (int i = 0; i < 3; ++i)
 #pragma unroll
             for (int jn = 0; jn < 2; ++jn)
-              acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[jn], acc[i][jn], 0, 0, 0);
+              acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[pb][i], bv[pb][jn], acc[i][jn], 0, 0, 0);
         }
-      } else {
-        f32x4 av0[3], av1[3], bv0[2], bv1[2];
+      }
+    } else {
+      constexpr int NG = ROWB / 64;
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          av0[i] = *reinterpret_cast<const f32x4*>(base + aoff[j][i]);
-          av1[i] = *reinterpret_cast<const f32x4*>(base + (aoff[j][i] ^ 16));
+      for (int j = 0; j < TAPS; ++j) {
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          f32x4 av0[3], av1[3], bv0[2], bv1[2];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            av0[i] = *reinterpret_cast<const f32x4*>(base + (aoff[j][i] ^ (g << 6)));
+            av1[i] = *reinterpret_cast<const f32x4*>(base + (aoff[j][i] ^ (g << 6) ^ 16));
+          }
+#pragma unroll
+          for (int jn = 0; jn < 2; ++jn) {
+            bv0[jn] = *reinterpret_cast<const f32x4*>(base + ((boff[jn] + j * kNT * ROWB) ^ (g << 6)));
+            bv1[jn] = *reinterpret_cast<const f32x4*>(base + ((boff[jn] + j * kNT * ROWB) ^ (g << 6) ^ 16));
+          }
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+              for (int jn = 0; jn < 2; ++jn)
+                acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av0[i][s4], bv0[jn][s4], acc[i][jn], 0, 0, 0);
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+              for (int jn = 0; jn < 2; ++jn)
+                acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av1[i][s4], bv1[jn][s4], acc[i][jn], 0, 0, 0);
         }
-#pragma unroll
-        for (int jn = 0; jn < 2; ++jn) {
-          bv0[jn] = *reinterpret_cast<const f32x4*>(base + boff[jn] + j * kNT * kRowB);
-          bv1[jn] = *reinterpret_cast<const f32x4*>(base + ((boff[jn] + j * kNT * kRowB) ^ 16));
-        }
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-          for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int jn = 0; jn < 2; ++jn)
-              acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av0[i][s4], bv0[jn][s4], acc[i][jn], 0, 0, 0);
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-          for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int jn = 0; jn < 2; ++jn)
-              acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av1[i][s4], bv1[jn][s4], acc[i][jn], 0, 0, 0);
       }
     }
-    if (kc + 1 < NC) sstore((kc + 1) & 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
   // ------------------------------- epilogue --------------------------------
   const int cout = a.cout;
-  auto map_add = [&](int b, int l, int n) -> float {
-    const int tac = a.tac ? a.tac[b] : 0;
-    const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[b];
-    float v = a.tmap ? a.tmap[((size_t)t * L + l) * cout + n] : a.bias[n];
-    if (a.cmap) v += a.cmap[((size_t)tac * L + l) * cout + n];
-    return v;
-  };
-
   if constexpr (EPI != EPI_FINAL) {
+    // accumulators -> fp32 C tile in LDS -> row-wise: + maps (float4), act, 16-B stores
+    float* ct = reinterpret_cast<float*>(smem);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < 3; ++i)
 #pragma unroll
-      for (int jn = 0; jn < 2; ++jn) {
-        const int n = n_tile * kNT + wn * 64 + jn * 32 + lr;
+      for (int jn = 0; jn < 2; ++jn)
 #pragma unroll
-        for (int rg = 0; rg < 16; rg += 2) {
-          const int r = wm * 96 + i * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * h;  // even row
-          const int s = r / L, l = r - s * L, b = m0 + s;
-          if (b < B) {
-            float v0 = acc[i][jn][rg] + map_add(b, l, n);
-            float v1 = acc[i][jn][rg + 1] + map_add(b, l + 1, n);
-            if constexpr (EPI != EPI_LIN) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); }
-            a.out[((size_t)b * L + l) * cout + n] = from_f<T>(v0);
-            a.out[((size_t)b * L + l + 1) * cout + n] = from_f<T>(v1);
-            if constexpr (EPI == EPI_POOL)
-              a.out_pool[((size_t)b * (L / 2) + (l >> 1)) * cout + n] = from_f<T>(fmaxf(v0, v1));
-          }
+        for (int rg = 0; rg < 16; ++rg) {
+          const int r = wm * 96 + i * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * h;
+          ct[r * G::CT_LD + wn * 64 + jn * 32 + lr] = acc[i][jn][rg];
         }
+    __syncthreads();
+    const int cg = tid & 15;                 // 8-column group
+    const int nloc = cg * 8, n = n_tile * kNT + nloc;
+    for (int rp = tid >> 4; rp < kMT / 2; rp += kThreads / 16) {
+      const int r = 2 * rp;
+      const int s = r / L, l = r - s * L, b = m0 + s;
+      if (b >= B) continue;
+      const int tac = a.tac ? a.tac[b] : 0;
+      const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[b];
+      float v[2][8];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const f32x4 c0v = *reinterpret_cast<const f32x4*>(ct + (r + e) * G::CT_LD + nloc);
+        const f32x4 c1v = *reinterpret_cast<const f32x4*>(ct + (r + e) * G::CT_LD + nloc + 4);
+        f32x4 m0v, m1v;
+        if (a.tmap) {
+          const float* mp = a.tmap + ((size_t)t * L + l + e) * cout + n;
+          m0v = *reinterpret_cast<const f32x4*>(mp);
+          m1v = *reinterpret_cast<const f32x4*>(mp + 4);
+        } else {
+          m0v = *reinterpret_cast<const f32x4*>(a.bias + n);
+          m1v = *reinterpret_cast<const f32x4*>(a.bias + n + 4);
+        }
+        if (a.cmap) {
+          const float* cp = a.cmap + ((size_t)tac * L + l + e) * cout + n;
+          m0v += *reinterpret_cast<const f32x4*>(cp);
+          m1v += *reinterpret_cast<const f32x4*>(cp + 4);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          v[e][q] = c0v[q] + m0v[q];
+          v[e][4 + q] = c1v[q] + m1v[q];
+        }
+        if constexpr (EPI != EPI_LIN) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[e][q] = fmaxf(v[e][q], 0.f);
+        }
+        Vec8<T>::store(a.out + ((size_t)b * L + l + e) * cout + n, v[e]);
+      }
+      if constexpr (EPI == EPI_POOL) {
+        float pv[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) pv[q] = fmaxf(v[0][q], v[1][q]);
+        Vec8<T>::store(a.out_pool + ((size_t)b * (L / 2) + (l >> 1)) * cout + n, pv);
       }
     }
   } else {
@@ -339,7 +407,13 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
           const int r = wm * 96 + i * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * h;
           const int s = r / L, l = r - s * L, b = m0 + s;
           float v = 0.f;
-          if (b < B) v = fmaxf(acc[i][jn][rg] + map_add(b, l, n), 0.f);
+          if (b < B) {
+            const int tac = a.tac ? a.tac[b] : 0;
+            const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[b];
+            float m = a.tmap ? a.tmap[((size_t)t * L + l) * cout + n] : a.bias[n];
+            if (a.cmap) m += a.cmap[((size_t)tac * L + l) * cout + n];
+            v = fmaxf(acc[i][jn][rg] + m, 0.f);
+          }
           fin[r * G::FIN_LD + n] = v;
         }
       }
@@ -394,9 +468,15 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
 // Writes the skip s0 (B*48 x 128) and the pooled p0 (B*24 x 128).
 // ---------------------------------------------------------------------------
 template <typename T>
-__global__ __launch_bounds__(128) void down0_kernel(Down0Args a) {
-  const int b = blockIdx.x / 24, lp = blockIdx.x - b * 24;
-  const int n = threadIdx.x;
+__global__ __launch_bounds__(256) void down0_kernel(Down0Args a) {
+  __shared__ __attribute__((aligned(16))) float w[6 * 2 * 128];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 6 * 2 * 128; i += 256) w[i] = a.w0[i];
+  __syncthreads();
+  const int pos = blockIdx.x * 16 + (tid >> 4);   // (sample, pooled position)
+  if (pos >= a.B * 24) return;
+  const int b = pos / 24, lp = pos - b * 24;
+  const int n0 = (tid & 15) * 8;
   const int l0 = 2 * lp;
   const float* xb = a.x + (size_t)b * 96;
   float xv[7][2];
@@ -409,25 +489,36 @@ __global__ __launch_bounds__(128) void down0_kernel(Down0Args a) {
   }
   const int tac = a.tac ? a.tac[b] : 0;
   const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[b];
-  float v[2];
+  float v[2][8];
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
     const int l = l0 + e;
-    float acc = 0.f;
+    const float* tm = a.tmap + ((size_t)t * 48 + l) * 128 + n0;
+    const float* cm = a.cmap + ((size_t)tac * 48 + l) * 128 + n0;
+    f32x4 m0 = *reinterpret_cast<const f32x4*>(tm) + *reinterpret_cast<const f32x4*>(cm);
+    f32x4 m1 = *reinterpret_cast<const f32x4*>(tm + 4) + *reinterpret_cast<const f32x4*>(cm + 4);
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
-      acc = fmaf(a.w0[(j * 2 + 0) * 128 + n], xv[e + j][0], acc);
-      acc = fmaf(a.w0[(j * 2 + 1) * 128 + n], xv[e + j][1], acc);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const f32x4 w0 = *reinterpret_cast<const f32x4*>(w + (j * 2 + c) * 128 + n0);
+        const f32x4 w1 = *reinterpret_cast<const f32x4*>(w + (j * 2 + c) * 128 + n0 + 4);
+        acc0 += w0 * xv[e + j][c];
+        acc1 += w1 * xv[e + j][c];
+      }
     }
-    acc += a.tmap[((size_t)t * 48 + l) * 128 + n];
-    acc += a.cmap[((size_t)tac * 48 + l) * 128 + n];
-    v[e] = fmaxf(acc, 0.f);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[e][q] = fmaxf(acc0[q] + m0[q], 0.f);
+      v[e][4 + q] = fmaxf(acc1[q] + m1[q], 0.f);
+    }
+    Vec8<T>::store(reinterpret_cast<T*>(a.s0) + ((size_t)b * 48 + l) * 128 + n0, v[e]);
   }
-  T* s0 = reinterpret_cast<T*>(a.s0);
-  T* p0 = reinterpret_cast<T*>(a.p0);
-  s0[((size_t)b * 48 + l0) * 128 + n] = from_f<T>(v[0]);
-  s0[((size_t)b * 48 + l0 + 1) * 128 + n] = from_f<T>(v[1]);
-  p0[((size_t)b * 24 + lp) * 128 + n] = from_f<T>(fmaxf(v[0], v[1]));
+  float pv[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) pv[q] = fmaxf(v[0][q], v[1][q]);
+  Vec8<T>::store(reinterpret_cast<T*>(a.p0) + ((size_t)b * 24 + lp) * 128 + n0, pv);
 }
 
 // ---------------------------------------------------------------------------
@@ -540,14 +631,14 @@ __global__ void posterior_stats_kernel(const float* x0, const int* tac, int B, i
 // ---------------------------------------------------------------------------
 template <typename T, int L, bool UPS, int TAPS, int PADL, int EPI>
 static hipError_t launch_one(const ConvArgs<T>& a, hipStream_t s) {
-  using G = ConvGeom<T, L, UPS, TAPS, PADL, EPI>;
-  constexpr int KC = TileCfg<T>::KC;
+  constexpr int ROWB = conv_rowb<T>(TAPS);
+  using G = ConvGeom<T, L, UPS, TAPS, PADL, EPI, ROWB>;
   if (a.B <= 0) return hipSuccess;
-  if (a.cout % kNT != 0 || a.c1 % KC != 0 || a.c2 % KC != 0) return hipErrorInvalidValue;
+  if (a.cout % kNT != 0 || a.c1 % G::KC != 0 || a.c2 % G::KC != 0) return hipErrorInvalidValue;
   if (EPI == EPI_FINAL && a.cout != kNT) return hipErrorInvalidValue;
   const int nM = (a.B + G::S - 1) / G::S;
   const int total = nM * (a.cout / kNT);
-  hipLaunchKernelGGL((conv_kernel<T, L, UPS, TAPS, PADL, EPI>), dim3(total), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL((conv_kernel<T, L, UPS, TAPS, PADL, EPI, ROWB>), dim3(total), dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 
@@ -570,7 +661,7 @@ hipError_t launch_conv(int kind, const ConvArgs<T>& a, hipStream_t s) {
 template <typename T>
 hipError_t launch_down0(const Down0Args& a, hipStream_t s) {
   if (a.B <= 0) return hipSuccess;
-  hipLaunchKernelGGL(down0_kernel<T>, dim3(a.B * 24), dim3(128), 0, s, a);
+  hipLaunchKernelGGL(down0_kernel<T>, dim3((a.B * 24 + 15) / 16), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -1,0 +1,11 @@
+# GPU round-trip: parity tests, bench, rocprofv3 kernel stats.  Usage: bash scripts/gpu_test_bench.sh TAG
+set -o pipefail
+TAG=${1:-run}
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out/$TAG
+timeout -k 10 600 python -m pytest tests -q -m gpu -p no:cacheprovider > gpurun_out/$TAG/pytest.log 2>&1
+echo "pytest exit $?" >> gpurun_out/$TAG/pytest.log
+timeout -k 10 400 python bench.py > gpurun_out/$TAG/bench.json 2> gpurun_out/$TAG/bench.err && \
+timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/$TAG/prof -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 2 --no-cpu-baseline > gpurun_out/$TAG/bench_prof.log 2>&1
+echo EXIT $?
