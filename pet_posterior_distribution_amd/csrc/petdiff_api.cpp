@@ -218,8 +218,9 @@ namespace {
 template <typename T, typename H>
 int pack_conv(petdiff_ctx* h, const std::vector<float>& wk_host, int li) {
   const ConvLayer& cl = kConv[li];
-  const int ROWB = conv_rowb<T>(cl.taps);
-  const int KC = conv_kc<T>(cl.taps);
+  const int ROWB = layer_tile(cl.kind).rowb;
+  const int KC = layer_kc<T>(cl.kind);
+  const int NT = layer_ntile(cl.kind);
   const int CPR = ROWB / 16;
   const int EPC = 16 / (int)sizeof(T);
   const Spec* sk = nullptr;
@@ -232,21 +233,22 @@ int pack_conv(petdiff_ctx* h, const std::vector<float>& wk_host, int li) {
   const float* wk = wk_host.data() + sk->off;
   const float* wr = sr ? wk_host.data() + sr->off : nullptr;
   if (cl.cin_x % KC != 0) return fail(PETDIFF_ERR_UNSUPPORTED, "channel count not a multiple of the K chunk");
-  const int NC = cl.cin_x / KC, nNT = cl.cout / kNT;
-  // [n_tile][chunk][tap][n (128)][CPR x 16-B pieces], piece index XOR-swizzled by n
+  if (cl.cout % NT != 0) return fail(PETDIFF_ERR_UNSUPPORTED, "cout not a multiple of the N tile");
+  const int NC = cl.cin_x / KC, nNT = cl.cout / NT;
+  // [n_tile][chunk][tap][n (NT)][CPR x 16-B pieces], piece index XOR-swizzled by n
   // exactly like ConvGeom::key so a linear LDS-DMA copy yields the swizzled image.
-  std::vector<H> out((size_t)nNT * NC * cl.taps * kNT * KC);
+  std::vector<H> out((size_t)nNT * NC * cl.taps * NT * KC);
   size_t q = 0;
   for (int nt = 0; nt < nNT; ++nt)
     for (int kc = 0; kc < NC; ++kc)
       for (int j = 0; j < cl.taps; ++j)
-        for (int n = 0; n < kNT; ++n)
+        for (int n = 0; n < NT; ++n)
           for (int p = 0; p < CPR; ++p) {
             const int key = CPR == 4 ? ((n >> 2) & 3) : ((n >> 1) & 7);
             const int c = p ^ key;
             for (int e = 0; e < EPC; ++e) {
               const int ci = cl.xoff + kc * KC + c * EPC + e;
-              const int co = nt * kNT + n;
+              const int co = nt * NT + n;
               float v = wk[((size_t)j * cl.cin_full + ci) * cl.cout + co];
               if (wr && j == cl.padl) v += wr[(size_t)ci * cl.cout + co];
               if constexpr (sizeof(H) == 2) out[q++] = f2bf(v);

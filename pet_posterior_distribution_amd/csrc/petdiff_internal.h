@@ -10,15 +10,7 @@ namespace petdiff {
 typedef __bf16 bf16;
 
 // Tile geometry of the implicit-GEMM Conv1D kernel (see DESIGN.md "conv kernel").
-constexpr int kMT = 192;      // output rows (sample x position) per workgroup
-constexpr int kNT = 128;      // output channels per workgroup
-constexpr int kThreads = 256; // 4 waves: 2 (M) x 2 (N), 96 x 64 per wave
-// Bytes of input channels per K chunk (one LDS row): 64 B for the 6-tap convs
-// (two stages of 6 taps x 128 x 64 B fit LDS), 128 B for the 2-tap up-convs.
-template <typename T>
-constexpr int conv_rowb(int taps) { return taps == 2 ? 128 : 64; }
-template <typename T>
-constexpr int conv_kc(int taps) { return conv_rowb<T>(taps) / (int)sizeof(T); }
+constexpr int kThreads = 256; // 4 waves; every wave owns a 96 x 64 output block (3 x 2 MFMA 32x32)
 
 // Epilogue kinds
 enum Epi : int {
@@ -105,5 +97,20 @@ enum LayerKind : int {
   LK_DOWN1 = 0, LK_DOWN2, LK_DOWN3, LK_UP0_CONV2, LK_UP0_BLOCK, LK_UP1_CONV2, LK_UP1_BLOCK,
   LK_UP2_CONV2, LK_UP2_BLOCK, kNumConvLayers
 };
+
+// Per-layer tile configuration, shared by the kernels and the host weight packer.
+//   wm x wn waves (wm*wn == 4): output tile (96*wm) rows x (64*wn) channels;
+//   stages: LDS ring depth of the K loop; rowb: bytes of input channels per K chunk.
+struct TileCfg {
+  int wm, wn, stages, rowb;
+};
+constexpr TileCfg layer_tile(int kind) {
+  return kind == LK_UP2_BLOCK ? TileCfg{2, 2, 2, 64}          // final conv needs all 128 channels
+         : (kind == LK_UP0_CONV2 || kind == LK_UP1_CONV2 || kind == LK_UP2_CONV2) ? TileCfg{4, 1, 3, 128}
+                                                                                  : TileCfg{4, 1, 3, 64};
+}
+constexpr int layer_ntile(int kind) { return 64 * layer_tile(kind).wn; }
+template <typename T>
+constexpr int layer_kc(int kind) { return layer_tile(kind).rowb / (int)sizeof(T); }
 
 }  // namespace petdiff

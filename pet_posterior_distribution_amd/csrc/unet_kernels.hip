@@ -57,6 +57,19 @@ __device__ __forceinline__ float philox_normal(unsigned long long seed, unsigned
   return (float)(which == 0 ? r * cos(ang) : r * sin(ang));
 }
 
+__device__ __forceinline__ void philox_normal2(unsigned long long seed, unsigned long long g, int step, int roi,
+                                               float* z) {
+  uint32_t c[4] = {(uint32_t)roi, (uint32_t)step, (uint32_t)(g & 0xffffffffull), (uint32_t)(g >> 32)};
+  philox4x32_10(c, (uint32_t)(seed & 0xffffffffull), (uint32_t)(seed >> 32));
+  const double u1 = ((double)c[0] + 1.0) * 2.3283064365386963e-10;
+  const double u2 = ((double)c[1] + 0.5) * 2.3283064365386963e-10;
+  const double r = sqrt(-2.0 * log(u1));
+  double sn, cs;
+  sincos(6.283185307179586 * u2, &sn, &cs);
+  z[0] = (float)(r * cs);
+  z[1] = (float)(r * sn);
+}
+
 // ---------------------------------------------------------------------------
 // p_sample epilogue (diffusion_model.py:424-496, 651-663), fp32, no FMA
 // contraction so every op rounds like the TF graph.
@@ -110,15 +123,34 @@ __device__ __forceinline__ void p_sample_elem(const FinalArgs& f, int t, float x
 }
 
 // ---------------------------------------------------------------------------
-// Implicit-GEMM Conv1D on MFMA.  See DESIGN.md for the tiling.
-//   M tile = 192 rows = S whole samples, N tile = 128 channels, 4 waves (2x2),
-//   96 x 64 per wave (3 x 2 MFMA 32x32 tiles).  K loop over chunks of
-//   ROWB bytes of input channels; per chunk all TAPS taps are served from one
-//   LDS copy of the chunk's input rows.
+// Implicit-GEMM Conv1D on MFMA.  See DESIGN.md "conv kernel".
+//   Output tile MT = 96*WM rows (= S whole samples) x NT = 64*WN channels,
+//   4 waves, each owning 96 x 64 (3 x 2 MFMA 32x32 tiles).  The K loop walks
+//   chunks of ROWB bytes of input channels through a STAGES-deep LDS ring
+//   filled by LDS-DMA; every tap of a chunk is served from ONE LDS copy of the
+//   chunk's input rows (tap = row shift; out-of-range rows read a zero row).
 // ---------------------------------------------------------------------------
-template <typename T, int L, bool UPS, int TAPS, int PADL, int EPI, int ROWB>
+template <int KIND> struct LayerShape;
+//                                  L   UPS   TAPS PADL EPI
+template <> struct LayerShape<LK_DOWN1> { static constexpr int L = 24, TAPS = 6, PADL = 2, EPI = EPI_POOL; static constexpr bool UPS = false; };
+template <> struct LayerShape<LK_DOWN2> { static constexpr int L = 12, TAPS = 6, PADL = 2, EPI = EPI_POOL; static constexpr bool UPS = false; };
+template <> struct LayerShape<LK_DOWN3> { static constexpr int L = 6, TAPS = 6, PADL = 2, EPI = EPI_RELU; static constexpr bool UPS = false; };
+template <> struct LayerShape<LK_UP0_CONV2> { static constexpr int L = 12, TAPS = 2, PADL = 0, EPI = EPI_LIN; static constexpr bool UPS = true; };
+template <> struct LayerShape<LK_UP0_BLOCK> { static constexpr int L = 12, TAPS = 6, PADL = 2, EPI = EPI_RELU; static constexpr bool UPS = false; };
+template <> struct LayerShape<LK_UP1_CONV2> { static constexpr int L = 24, TAPS = 2, PADL = 0, EPI = EPI_LIN; static constexpr bool UPS = true; };
+template <> struct LayerShape<LK_UP1_BLOCK> { static constexpr int L = 24, TAPS = 6, PADL = 2, EPI = EPI_RELU; static constexpr bool UPS = false; };
+template <> struct LayerShape<LK_UP2_CONV2> { static constexpr int L = 48, TAPS = 2, PADL = 0, EPI = EPI_LIN; static constexpr bool UPS = true; };
+template <> struct LayerShape<LK_UP2_BLOCK> { static constexpr int L = 48, TAPS = 6, PADL = 2, EPI = EPI_FINAL; static constexpr bool UPS = false; };
+
+template <typename T, int KIND>
 struct ConvGeom {
-  static constexpr int S = kMT / L;                 // samples per workgroup
+  using Sh = LayerShape<KIND>;
+  static constexpr int L = Sh::L, TAPS = Sh::TAPS, PADL = Sh::PADL, EPI = Sh::EPI;
+  static constexpr bool UPS = Sh::UPS;
+  static constexpr TileCfg TC = layer_tile(KIND);
+  static constexpr int WM = TC.wm, WN = TC.wn, STAGES = TC.stages, ROWB = TC.rowb;
+  static constexpr int MT = 96 * WM, NT = 64 * WN;
+  static constexpr int S = MT / L;                  // samples per workgroup
   static constexpr int LIN = UPS ? L / 2 : L;       // input rows per sample
   static constexpr int AROWS = S * LIN;
   static constexpr int ZROW = AROWS;                // always-zero LDS row
@@ -126,62 +158,85 @@ struct ConvGeom {
   static constexpr int KC = ROWB / (int)sizeof(T);  // input channels per chunk
   static constexpr int EPC = 16 / (int)sizeof(T);   // elements per 16-B piece
   static constexpr int A_BYTES = ((AROWS + 1) * ROWB + 255) / 256 * 256;
-  static constexpr int B_BYTES = TAPS * kNT * ROWB;
+  static constexpr int B_BYTES = TAPS * NT * ROWB;
   static constexpr int STAGE = A_BYTES + B_BYTES;
   static constexpr int APIECES = AROWS * CPR;
   static constexpr int APT = (APIECES + kThreads - 1) / kThreads;
   static constexpr int BPT = B_BYTES / 16 / kThreads;
-  static constexpr int CT_LD = kNT + 4;             // fp32 C tile row (non-final epilogue)
-  static constexpr int FIN_LD = 129;                 // fp32 C tile row (final epilogue)
-  static constexpr int EPI_BYTES = (EPI == EPI_FINAL) ? kMT * FIN_LD * 4 + 128 * 4 * 4 + 64 : kMT * CT_LD * 4;
-  static constexpr int SMEM = EPI_BYTES > 2 * STAGE ? EPI_BYTES : 2 * STAGE;
-  static_assert(kMT % L == 0, "tile must hold whole samples");
+  static constexpr bool AFULL = (APIECES % kThreads) == 0;
+  static constexpr int PER = APT + BPT;             // LDS-DMA instructions per wave per chunk
+  static constexpr int CT_LD = NT + 4;              // fp32 C tile row (non-final epilogue)
+  static constexpr int FIN_LD = 132;                // fp32 C tile row (final epilogue, 16-B aligned)
+  static constexpr int EPI_BYTES = (EPI == EPI_FINAL) ? MT * FIN_LD * 4 + 128 * 4 * 4 + 64 : MT * CT_LD * 4;
+  static constexpr int SMEM = EPI_BYTES > STAGES * STAGE ? EPI_BYTES : STAGES * STAGE;
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(MT % L == 0, "tile must hold whole samples");
   static_assert(B_BYTES % (16 * kThreads) == 0, "B tile split");
   static_assert(ROWB == 64 || ROWB == 128, "row width");
+  static_assert(STAGES == 2 || (STAGES == 3 && AFULL), "3-stage ring needs uniform per-wave DMA counts");
+  static_assert(PER < 64, "vmcnt range");
   static_assert(SMEM <= 160 * 1024, "LDS budget");
+  static_assert(EPI != EPI_FINAL || NT == 128, "final conv needs every channel in the tile");
   // XOR key of the 16-B piece index within a row: conflict-free ds_read_b128 for
   // 16 consecutive rows (lane groups of MI355X_MICROARCH.md LDS table)
   static __device__ __forceinline__ int key(int row) { return CPR == 4 ? ((row >> 2) & 3) : ((row >> 1) & 7); }
 };
 
-// Global -> LDS staging of chunk kc into stage buf by LDS-DMA
-// (global_load_lds_dwordx4).  Piece p of a stage lands at byte 16*p; the pieces
-// of one wave instruction are the 64 consecutive p = q*256 + wave*64 + lane, so
-// the LDS destination is wave-uniform base + lane*16 and the XOR swizzle lives
-// in the SOURCE address.
-template <typename T, int L, bool UPS, int TAPS, int PADL, int EPI, int ROWB>
-__device__ __forceinline__ void stage_issue(const ConvArgs<T>& a, char* smem, int kc, int buf, int n1, int NC,
-                                            int m0, int n_tile, int wv, int lane) {
-  using G = ConvGeom<T, L, UPS, TAPS, PADL, EPI, ROWB>;
-  const T* src;
-  int stride, ch;
-  if (kc < n1) { src = a.src1; stride = a.c1; ch = kc * G::KC; }
-  else { src = a.src2; stride = a.c2; ch = (kc - n1) * G::KC; }
-  char* sbase = smem + buf * G::STAGE;
+// Global -> LDS staging by LDS-DMA (global_load_lds_dwordx4).  Piece p of a
+// stage lands at byte 16*p; the pieces of one wave instruction are the 64
+// consecutive p = q*256 + wave*64 + lane, so the LDS destination is
+// wave-uniform base + lane*16 and the XOR swizzle lives in the SOURCE address.
+// The per-thread source offsets are computed once; piece k of chunk kc is
+// issued by piece(k, ...) so the issues can be interleaved with the MFMAs.
+template <typename T, int KIND>
+struct DmaPlan {
+  using G = ConvGeom<T, KIND>;
+  int aoff1[G::APT], aoff2[G::APT];   // element offsets of this lane's A pieces in src1 / src2
+  const char* wbase;                  // this lane's first B piece of chunk 0
+  int n1, wv;
+
+  __device__ __forceinline__ void init(const ConvArgs<T>& a, int m0, int n_tile, int NC, int wv_, int lane) {
+    n1 = a.c1 / G::KC;
+    wv = wv_;
 #pragma unroll
-  for (int qq = 0; qq < G::APT; ++qq) {
-    const int p0 = qq * kThreads + wv * 64;
-    if (p0 < G::APIECES) {
-      const int p = p0 + lane;
-      if (p < G::APIECES) {
-        const int row = p / G::CPR, cp = p - row * G::CPR;
-        const int c = cp ^ G::key(row);
-        const int s = row / G::LIN, li = row - s * G::LIN;
-        const int b = min(m0 + s, a.B - 1);   // rows of absent samples only feed unstored outputs
-        const T* g = src + (size_t)(b * G::LIN + li) * stride + ch + c * G::EPC;
-        __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(sbase + p0 * 16), 16, 0, 0);
+    for (int qq = 0; qq < G::APT; ++qq) {
+      int p = qq * kThreads + wv * 64 + lane;
+      if (p >= G::APIECES) p = G::APIECES - 1;   // inactive lanes of a partial last instruction
+      const int row = p / G::CPR, cp = p - row * G::CPR;
+      const int c = cp ^ G::key(row);
+      const int s = row / G::LIN, li = row - s * G::LIN;
+      const int b = min(m0 + s, a.B - 1);        // rows of absent samples only feed unstored outputs
+      aoff1[qq] = (b * G::LIN + li) * a.c1 + c * G::EPC;
+      aoff2[qq] = (b * G::LIN + li) * a.c2 + c * G::EPC;
+    }
+    wbase = reinterpret_cast<const char*>(a.wpack) + (size_t)n_tile * NC * G::B_BYTES + (size_t)(wv * 64 + lane) * 16;
+  }
+
+  // issue DMA piece k (0..PER-1) of chunk kc into stage buf
+  __device__ __forceinline__ void piece(const ConvArgs<T>& a, char* smem, int k, int kc, int buf, int lane) const {
+    char* sbase = smem + buf * G::STAGE;
+    if (k < G::APT) {
+      const int p0 = k * kThreads + wv * 64;
+      if (G::AFULL || p0 < G::APIECES) {
+        if (G::AFULL || p0 + lane < G::APIECES) {
+          const T* g = kc < n1 ? a.src1 + aoff1[k] + kc * G::KC : a.src2 + aoff2[k] + (kc - n1) * G::KC;
+          __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(sbase + p0 * 16), 16, 0, 0);
+        }
       }
+    } else {
+      const int qq = k - G::APT;
+      const int p0 = qq * kThreads + wv * 64;
+      __builtin_amdgcn_global_load_lds(wbase + (size_t)kc * G::B_BYTES + qq * kThreads * 16,
+                                       (__attribute__((address_space(3))) void*)(sbase + G::A_BYTES + p0 * 16), 16,
+                                       0, 0);
     }
   }
-  const char* wp = reinterpret_cast<const char*>(a.wpack) + (size_t)(n_tile * NC + kc) * G::B_BYTES;
+
+  __device__ __forceinline__ void all(const ConvArgs<T>& a, char* smem, int kc, int buf, int lane) const {
 #pragma unroll
-  for (int qq = 0; qq < G::BPT; ++qq) {
-    const int p0 = qq * kThreads + wv * 64;
-    __builtin_amdgcn_global_load_lds(wp + (size_t)(p0 + lane) * 16,
-                                     (__attribute__((address_space(3))) void*)(sbase + G::A_BYTES + p0 * 16), 16,
-                                     0, 0);
+    for (int k = 0; k < G::PER; ++k) piece(a, smem, k, kc, buf, lane);
   }
-}
+};
 
 template <typename T> struct Vec8;
 template <> struct Vec8<bf16> {
@@ -199,32 +254,49 @@ template <> struct Vec8<float> {
   }
 };
 
-template <typename T, int L, bool UPS, int TAPS, int PADL, int EPI, int ROWB>
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// LDS-DMA of this wave retired to vmcnt <= N, own LDS reads done, then a bare
+// s_barrier (a __syncthreads() would drain every in-flight DMA: vmcnt(0)).
+template <int N>
+__device__ __forceinline__ void ring_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <typename T, int KIND>
 __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
-  using G = ConvGeom<T, L, UPS, TAPS, PADL, EPI, ROWB>;
+  using G = ConvGeom<T, KIND>;
+  constexpr int L = G::L, TAPS = G::TAPS, PADL = G::PADL, EPI = G::EPI, ROWB = G::ROWB, NT = G::NT;
+  constexpr bool UPS = G::UPS;
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  const int lane = tid & 63, w = tid >> 6;
+  const int wm = w / G::WN, wn = w - wm * G::WN;
   const int h = lane >> 5, lr = lane & 31;
 
-  // XCD-aware bijective block remap: the blocks sharing an XCD (bid % 8) get a
-  // contiguous slot range, i.e. (mostly) the same N tile -> weight slice stays in that L2.
+  // XCD-aware bijective block remap.  Blocks sharing an XCD (bid % 8) get a
+  // contiguous slot range; slots run N-fastest, so one XCD holds few M tiles
+  // (their activation rows stay in its L2) and streams the N tiles' weights.
   const int B = a.B;
   const int nM = (B + G::S - 1) / G::S;
-  const int nN = a.cout / kNT;
+  const int nN = a.cout / NT;
   const int total = nM * nN;
   const int bid = blockIdx.x;
   const int xcd = bid & 7, loc = bid >> 3, q8 = total >> 3, r8 = total & 7;
   const int slot = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
-  const int n_tile = slot / nM, m_tile = slot - n_tile * nM;
+  const int m_tile = slot / nN, n_tile = slot - m_tile * nN;
   const int m0 = m_tile * G::S;
 
-  const int n1 = a.c1 / G::KC;
-  const int NC = n1 + a.c2 / G::KC;
+  const int NC = a.c1 / G::KC + a.c2 / G::KC;
 
-  // zero row of both stages
-  if (tid < 2 * G::CPR) {
+  // zero row of every stage
+  if (tid < G::STAGES * G::CPR) {
     const int st = tid / G::CPR, pc = tid - st * G::CPR;
     *reinterpret_cast<uint4*>(smem + st * G::STAGE + G::ZROW * ROWB + pc * 16) = make_uint4(0, 0, 0, 0);
   }
@@ -261,18 +333,17 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][jn][e] = 0.f;
 
-  stage_issue<T, L, UPS, TAPS, PADL, EPI, ROWB>(a, smem, 0, 0, n1, NC, m0, n_tile, wv, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  DmaPlan<T, KIND> dma;
+  dma.init(a, m0, n_tile, NC, wv, lane);
 
-  for (int kc = 0; kc < NC; ++kc) {
-    if (kc + 1 < NC)
-      stage_issue<T, L, UPS, TAPS, PADL, EPI, ROWB>(a, smem, kc + 1, (kc + 1) & 1, n1, NC, m0, n_tile, wv, lane);
-    const char* base = smem + (kc & 1) * G::STAGE;
+  // One chunk: TAPS x (ROWB/32 bf16 | ROWB/64 f32) MFMA steps.  The DMA pieces of
+  // chunk nkc (into stage nbuf) are issued spread over the steps (nkc < 0: none).
+  auto compute = [&](const char* base, int nkc, int nbuf) {
     if constexpr (sizeof(T) == 2) {
       // step = (tap j, 16-k group g); fragments of step+1 are read while step's MFMAs run
       constexpr int NG = ROWB / 32;
       constexpr int NS = TAPS * NG;
+      constexpr int PPS = (G::PER + NS - 1) / NS;   // DMA pieces per step
       bf16x8 av[2][3], bv[2][2];
 #pragma unroll
       for (int st = 0; st < NS + 1; ++st) {
@@ -282,7 +353,12 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
           for (int i = 0; i < 3; ++i) av[sb][i] = *reinterpret_cast<const bf16x8*>(base + (aoff[j][i] ^ (g << 5)));
 #pragma unroll
           for (int jn = 0; jn < 2; ++jn)
-            bv[sb][jn] = *reinterpret_cast<const bf16x8*>(base + ((boff[jn] + j * kNT * ROWB) ^ (g << 5)));
+            bv[sb][jn] = *reinterpret_cast<const bf16x8*>(base + ((boff[jn] + j * NT * ROWB) ^ (g << 5)));
+        }
+        if (nkc >= 0) {
+#pragma unroll
+          for (int u = 0; u < PPS; ++u)
+            if (st * PPS + u < G::PER) dma.piece(a, smem, st * PPS + u, nkc, nbuf, lane);
         }
         if (st > 0) {
           const int pb = (st - 1) & 1;
@@ -295,6 +371,8 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
       }
     } else {
       constexpr int NG = ROWB / 64;
+      constexpr int NS = TAPS * NG;
+      constexpr int PPS = (G::PER + NS - 1) / NS;
 #pragma unroll
       for (int j = 0; j < TAPS; ++j) {
 #pragma unroll
@@ -307,8 +385,14 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
           }
 #pragma unroll
           for (int jn = 0; jn < 2; ++jn) {
-            bv0[jn] = *reinterpret_cast<const f32x4*>(base + ((boff[jn] + j * kNT * ROWB) ^ (g << 6)));
-            bv1[jn] = *reinterpret_cast<const f32x4*>(base + ((boff[jn] + j * kNT * ROWB) ^ (g << 6) ^ 16));
+            bv0[jn] = *reinterpret_cast<const f32x4*>(base + ((boff[jn] + j * NT * ROWB) ^ (g << 6)));
+            bv1[jn] = *reinterpret_cast<const f32x4*>(base + ((boff[jn] + j * NT * ROWB) ^ (g << 6) ^ 16));
+          }
+          if (nkc >= 0) {
+            const int st = j * NG + g;
+#pragma unroll
+            for (int u = 0; u < PPS; ++u)
+              if (st * PPS + u < G::PER) dma.piece(a, smem, st * PPS + u, nkc, nbuf, lane);
           }
 #pragma unroll
           for (int s4 = 0; s4 < 4; ++s4)
@@ -327,14 +411,42 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
         }
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  if constexpr (G::STAGES == 2) {
+    dma.all(a, smem, 0, 0, lane);
+    wait_vmcnt<0>();
     __syncthreads();
+    for (int kc = 0; kc < NC; ++kc) {
+      compute(smem + (kc & 1) * G::STAGE, kc + 1 < NC ? kc + 1 : -1, (kc + 1) & 1);
+      wait_vmcnt<0>();
+      __syncthreads();
+    }
+  } else {
+    // 3-deep ring: chunk kc+2 is in flight while chunk kc is computed; the wait
+    // before each barrier retires chunk kc+1 only (counted vmcnt, never 0 mid-loop).
+    dma.all(a, smem, 0, 0, lane);
+    if (NC > 1) {
+      dma.all(a, smem, 1, 1, lane);
+      ring_barrier<G::PER>();
+    } else {
+      ring_barrier<0>();
+    }
+    int buf = 0;
+    for (int kc = 0; kc < NC; ++kc) {
+      const int nb = buf == 0 ? 2 : buf - 1;          // (kc + 2) % 3
+      const bool more = kc + 2 < NC;
+      compute(smem + buf * G::STAGE, more ? kc + 2 : -1, nb);
+      if (more) ring_barrier<G::PER>();
+      else ring_barrier<0>();
+      buf = buf == 2 ? 0 : buf + 1;
+    }
   }
 
   // ------------------------------- epilogue --------------------------------
   const int cout = a.cout;
   if constexpr (EPI != EPI_FINAL) {
-    // accumulators -> fp32 C tile in LDS -> row-wise: + maps (float4), act, 16-B stores
+    // accumulators -> fp32 C tile in LDS -> row pairs: + maps (float4), act, 16-B stores
     float* ct = reinterpret_cast<float*>(smem);
 #pragma unroll
     for (int i = 0; i < 3; ++i)
@@ -346,9 +458,10 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
           ct[r * G::CT_LD + wn * 64 + jn * 32 + lr] = acc[i][jn][rg];
         }
     __syncthreads();
-    const int cg = tid & 15;                 // 8-column group
-    const int nloc = cg * 8, n = n_tile * kNT + nloc;
-    for (int rp = tid >> 4; rp < kMT / 2; rp += kThreads / 16) {
+    constexpr int TPR = NT / 8;                 // threads per row (8 channels each)
+    const int cg = tid % TPR;
+    const int nloc = cg * 8, n = n_tile * NT + nloc;
+    for (int rp = tid / TPR; rp < G::MT / 2; rp += kThreads / TPR) {
       const int r = 2 * rp;
       const int s = r / L, l = r - s * L, b = m0 + s;
       if (b >= B) continue;
@@ -392,71 +505,80 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
       }
     }
   } else {
-    // up2 ConvBlock output (relu) -> LDS -> final 1x1 conv (networks.py:1074) -> p_sample
+    // up2 ConvBlock (relu(acc + bias)) -> final Conv1D 1x1 128 -> n_out (networks.py:1074)
+    // -> p_sample epilogue; one thread per output row.
     float* fin = reinterpret_cast<float*>(smem);
-    float* wfl = fin + kMT * G::FIN_LD;
+    float* wfl = fin + G::MT * G::FIN_LD;
     const FinalArgs& f = a.fin;
     const int n_out = f.n_out;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < 3; ++i)
 #pragma unroll
-      for (int jn = 0; jn < 2; ++jn) {
-        const int n = wn * 64 + jn * 32 + lr;
+      for (int jn = 0; jn < 2; ++jn)
 #pragma unroll
         for (int rg = 0; rg < 16; ++rg) {
           const int r = wm * 96 + i * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * h;
-          const int s = r / L, l = r - s * L, b = m0 + s;
-          float v = 0.f;
-          if (b < B) {
-            const int tac = a.tac ? a.tac[b] : 0;
-            const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[b];
-            float m = a.tmap ? a.tmap[((size_t)t * L + l) * cout + n] : a.bias[n];
-            if (a.cmap) m += a.cmap[((size_t)tac * L + l) * cout + n];
-            v = fmaxf(acc[i][jn][rg] + m, 0.f);
-          }
-          fin[r * G::FIN_LD + n] = v;
+          fin[r * G::FIN_LD + wn * 64 + jn * 32 + lr] = acc[i][jn][rg];
         }
-      }
+    // final kernel as [n][4] (zero-padded when n_out == 2) for float4 reads
+    for (int e = tid; e < 128 * 4; e += kThreads) {
+      const int nn = e >> 2, o = e & 3;
+      wfl[e] = o < n_out ? f.wf[nn * n_out + o] : 0.f;
     }
-    for (int e = tid; e < 128 * n_out; e += kThreads) wfl[e] = f.wf[e];
     __syncthreads();
-    if (f.net_out) {
-      for (int it = tid; it < kMT * n_out; it += kThreads) {
-        const int r = it / n_out, o = it - r * n_out;
-        const int s = r / L, l = r - s * L, b = m0 + s;
-        if (b >= B) continue;
-        float accf = 0.f;
-        for (int n = 0; n < 128; ++n) accf = fmaf(fin[r * G::FIN_LD + n], wfl[n * n_out + o], accf);
-        f.net_out[((size_t)b * L + l) * n_out + o] = accf + f.bf[o];
-      }
-    } else {
-      const unsigned long long seed = f.rng ? f.rng[0] : 0ull;
-      const unsigned long long goff = f.rng ? f.rng[1] : 0ull;
-      const int half = n_out / 2;   // eps channels = 2, var channels follow when learned
-      for (int it = tid; it < kMT * 2; it += kThreads) {
-        const int r = it >> 1, c = it & 1;
-        const int s = r / L, l = r - s * L, b = m0 + s;
-        if (b >= B) continue;
-        float mo = 0.f, vv = 0.f;
-        for (int n = 0; n < 128; ++n) mo = fmaf(fin[r * G::FIN_LD + n], wfl[n * n_out + c], mo);
-        mo += f.bf[c];
-        if (n_out == 4) {
-          for (int n = 0; n < 128; ++n) vv = fmaf(fin[r * G::FIN_LD + n], wfl[n * n_out + half + c], vv);
-          vv += f.bf[half + c];
+    for (int r = tid; r < G::MT; r += kThreads) {
+      const int s = r / L, l = r - s * L, b = m0 + s;
+      if (b >= B) continue;
+      const int tac = a.tac ? a.tac[b] : 0;
+      const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[b];
+      const float* mp = a.tmap ? a.tmap + ((size_t)t * L + l) * cout : nullptr;
+      const float* cp = a.cmap ? a.cmap + ((size_t)tac * L + l) * cout : nullptr;
+      f32x4 o4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int n = 0; n < 128; n += 4) {
+        f32x4 hv = *reinterpret_cast<const f32x4*>(fin + r * G::FIN_LD + n);
+        hv += mp ? *reinterpret_cast<const f32x4*>(mp + n) : *reinterpret_cast<const f32x4*>(a.bias + n);
+        if (cp) hv += *reinterpret_cast<const f32x4*>(cp + n);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float hq = fmaxf(hv[q], 0.f);
+          const f32x4 wq = *reinterpret_cast<const f32x4*>(wfl + (n + q) * 4);
+          o4[0] = fmaf(hq, wq[0], o4[0]);
+          o4[1] = fmaf(hq, wq[1], o4[1]);
+          o4[2] = fmaf(hq, wq[2], o4[2]);
+          o4[3] = fmaf(hq, wq[3], o4[3]);
         }
-        const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[b];
-        const size_t idx = ((size_t)b * L + l) * 2 + c;
-        const float x = f.x_t[idx];
-        const float z = f.z ? f.z[idx] : philox_normal(seed, goff + (unsigned long long)b, f.rng_step, l, c);
+      }
+      float o[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = o4[q] + (q < n_out ? f.bf[q] : 0.f);
+      if (f.net_out) {
+        for (int q = 0; q < n_out; ++q) f.net_out[((size_t)b * L + l) * n_out + q] = o[q];
+        continue;
+      }
+      // one Philox call yields the Box-Muller pair for both parameters of this ROI
+      float z[2];
+      const size_t idx = ((size_t)b * L + l) * 2;
+      if (f.z) {
+        z[0] = f.z[idx];
+        z[1] = f.z[idx + 1];
+      } else {
+        philox_normal2(f.rng[0], f.rng[1] + (unsigned long long)b, f.rng_step, l, z);
+      }
+      const int half = n_out / 2;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const float mo = o[c];
+        const float vv = n_out == 4 ? o[half + c] : 0.f;
         float mean, var, var_t;
-        p_sample_elem(f, t, x, mo, vv, z, &mean, &var, &var_t);
-        if (f.mean_out) f.mean_out[idx] = mean;
-        if (f.var_out) f.var_out[idx] = var;
-        if (f.var_tilde_out) f.var_tilde_out[idx] = var_t;
+        p_sample_elem(f, t, f.x_t[idx + c], mo, vv, z[c], &mean, &var, &var_t);
+        if (f.mean_out) f.mean_out[idx + c] = mean;
+        if (f.var_out) f.var_out[idx + c] = var;
+        if (f.var_tilde_out) f.var_tilde_out[idx + c] = var_t;
         if (f.x_next) {
           const float xn = mean + (f.flag_var_tilde ? var_t : var);
-          f.x_next[idx] = xn;
-          if (f.x_all) f.x_all[idx] = xn;
+          f.x_next[idx + c] = xn;
+          if (f.x_all) f.x_all[idx + c] = xn;
         }
       }
     }
@@ -629,31 +751,29 @@ __global__ void posterior_stats_kernel(const float* x0, const int* tac, int B, i
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
-template <typename T, int L, bool UPS, int TAPS, int PADL, int EPI>
+template <typename T, int KIND>
 static hipError_t launch_one(const ConvArgs<T>& a, hipStream_t s) {
-  constexpr int ROWB = conv_rowb<T>(TAPS);
-  using G = ConvGeom<T, L, UPS, TAPS, PADL, EPI, ROWB>;
+  using G = ConvGeom<T, KIND>;
   if (a.B <= 0) return hipSuccess;
-  if (a.cout % kNT != 0 || a.c1 % G::KC != 0 || a.c2 % G::KC != 0) return hipErrorInvalidValue;
-  if (EPI == EPI_FINAL && a.cout != kNT) return hipErrorInvalidValue;
+  if (a.cout % G::NT != 0 || a.c1 % G::KC != 0 || a.c2 % G::KC != 0) return hipErrorInvalidValue;
   const int nM = (a.B + G::S - 1) / G::S;
-  const int total = nM * (a.cout / kNT);
-  hipLaunchKernelGGL((conv_kernel<T, L, UPS, TAPS, PADL, EPI, ROWB>), dim3(total), dim3(kThreads), 0, s, a);
+  const int total = nM * (a.cout / G::NT);
+  hipLaunchKernelGGL((conv_kernel<T, KIND>), dim3(total), dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 
 template <typename T>
 hipError_t launch_conv(int kind, const ConvArgs<T>& a, hipStream_t s) {
   switch (kind) {
-    case LK_DOWN1: return launch_one<T, 24, false, 6, 2, EPI_POOL>(a, s);
-    case LK_DOWN2: return launch_one<T, 12, false, 6, 2, EPI_POOL>(a, s);
-    case LK_DOWN3: return launch_one<T, 6, false, 6, 2, EPI_RELU>(a, s);
-    case LK_UP0_CONV2: return launch_one<T, 12, true, 2, 0, EPI_LIN>(a, s);
-    case LK_UP0_BLOCK: return launch_one<T, 12, false, 6, 2, EPI_RELU>(a, s);
-    case LK_UP1_CONV2: return launch_one<T, 24, true, 2, 0, EPI_LIN>(a, s);
-    case LK_UP1_BLOCK: return launch_one<T, 24, false, 6, 2, EPI_RELU>(a, s);
-    case LK_UP2_CONV2: return launch_one<T, 48, true, 2, 0, EPI_LIN>(a, s);
-    case LK_UP2_BLOCK: return launch_one<T, 48, false, 6, 2, EPI_FINAL>(a, s);
+    case LK_DOWN1: return launch_one<T, LK_DOWN1>(a, s);
+    case LK_DOWN2: return launch_one<T, LK_DOWN2>(a, s);
+    case LK_DOWN3: return launch_one<T, LK_DOWN3>(a, s);
+    case LK_UP0_CONV2: return launch_one<T, LK_UP0_CONV2>(a, s);
+    case LK_UP0_BLOCK: return launch_one<T, LK_UP0_BLOCK>(a, s);
+    case LK_UP1_CONV2: return launch_one<T, LK_UP1_CONV2>(a, s);
+    case LK_UP1_BLOCK: return launch_one<T, LK_UP1_BLOCK>(a, s);
+    case LK_UP2_CONV2: return launch_one<T, LK_UP2_CONV2>(a, s);
+    case LK_UP2_BLOCK: return launch_one<T, LK_UP2_BLOCK>(a, s);
   }
   return hipErrorInvalidValue;
 }

@@ -1,0 +1,50 @@
+"""Summarise rocprofv3 --pmc passes: per-kernel mean counter value per dispatch.
+
+FETCH_SIZE is doubled (gfx950 tallies 128-B requests at 64 B: MI355X_MICROARCH.md HBM);
+FETCH_SIZE / WRITE_SIZE are in KB.  Usage: python scripts/pmc_summary.py gpurun_out/pmc1 [out.json]
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+LAYERS = ['down1', 'down2', 'down3', 'up0.conv2', 'up0.block', 'up1.conv2', 'up1.block', 'up2.conv2', 'up2.block']
+
+
+def short(name):
+    import re
+    m = re.search(r'conv_kernelI(?:DF16b|f)Li(\d)E', name)
+    if m:
+        return LAYERS[int(m.group(1))]
+    if 'down0_kernel' in name:
+        return 'down0'
+    return None
+
+
+def main(d, out=None):
+    vals = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(os.path.join(d, 'p*', 'run_counter_collection.csv')):
+        for r in csv.DictReader(open(f)):
+            k = short(r['Kernel_Name'])
+            if k is None:
+                continue
+            vals[k][r['Counter_Name']].append(float(r['Counter_Value']))
+    res = {}
+    for k, cs in vals.items():
+        res[k] = {c: sum(v) / len(v) for c, v in cs.items()}
+        if 'FETCH_SIZE' in res[k]:
+            res[k]['hbm_read_bytes_corrected'] = res[k]['FETCH_SIZE'] * 2 * 1024
+        if 'WRITE_SIZE' in res[k]:
+            res[k]['hbm_write_bytes'] = res[k]['WRITE_SIZE'] * 1024
+    for k in sorted(res):
+        print(k, {c: round(v, 1) for c, v in res[k].items()})
+    if out:
+        json.dump(res, open(out, 'w'), indent=1)
+    return res
+
+
+if __name__ == '__main__':
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
