@@ -19,6 +19,8 @@
 // The 1x1 residual conv is folded into the centre tap of the packed weights.
 #include "petdiff_internal.h"
 
+#include <type_traits>
+
 namespace petdiff {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -188,16 +190,39 @@ struct ConvGeom {
 // wave-uniform base + lane*16 and the XOR swizzle lives in the SOURCE address.
 // The per-thread source offsets are computed once; piece k of chunk kc is
 // issued by piece(k, ...) so the issues can be interleaved with the MFMAs.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+// MUBUF LDS-DMA (buffer_load_dwordx4 ... lds).  A MUBUF load, unlike the FLAT-encoded
+// global_load_lds, is not treated by the compiler's wait-count pass as a possible
+// LDS access through FLAT, so the ds_read waits in the MFMA loop stay counted.
+__device__ void llvm_amdgcn_raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) void* lds, int size,
+                                                int voffset, int soffset, int offset,
+                                                int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
+
+__device__ __forceinline__ i32x4 make_rsrc(const void* base, unsigned bytes) {
+  const unsigned long long p = reinterpret_cast<unsigned long long>(base);
+  i32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(p & 0xffffffffull));
+  r[1] = __builtin_amdgcn_readfirstlane((int)((p >> 32) & 0xffffull));   // stride 0
+  r[2] = __builtin_amdgcn_readfirstlane((int)bytes);                      // num_records (bytes)
+  r[3] = 0x00020000;                                                      // gfx9 raw buffer dword3
+  return r;
+}
+
 template <typename T, int KIND>
 struct DmaPlan {
   using G = ConvGeom<T, KIND>;
-  int aoff1[G::APT], aoff2[G::APT];   // element offsets of this lane's A pieces in src1 / src2
-  const char* wbase;                  // this lane's first B piece of chunk 0
-  int n1, wv;
+  i32x4 rs1, rs2, rsw;                // buffer resources: src1, src2, packed weights
+  int avoff1[G::APT], avoff2[G::APT]; // byte offsets of this lane's A pieces (chunk 0) in src1 / src2
+  int bvoff;                          // byte offset of this lane's B piece 0 within a chunk's B tile
+  int n1, wv, wbase;                  // wbase: byte offset of this tile's chunk 0 in the packed weights
 
   __device__ __forceinline__ void init(const ConvArgs<T>& a, int m0, int n_tile, int NC, int wv_, int lane) {
     n1 = a.c1 / G::KC;
     wv = wv_;
+    const unsigned rows = (unsigned)a.B * G::LIN;
+    rs1 = make_rsrc(a.src1, rows * (unsigned)a.c1 * (unsigned)sizeof(T));
+    rs2 = make_rsrc(a.src2 ? a.src2 : a.src1, rows * (unsigned)a.c2 * (unsigned)sizeof(T));
+    rsw = make_rsrc(a.wpack, (unsigned)(a.cout / G::NT) * (unsigned)NC * (unsigned)G::B_BYTES);
 #pragma unroll
     for (int qq = 0; qq < G::APT; ++qq) {
       int p = qq * kThreads + wv * 64 + lane;
@@ -206,35 +231,36 @@ struct DmaPlan {
       const int c = cp ^ G::key(row);
       const int s = row / G::LIN, li = row - s * G::LIN;
       const int b = min(m0 + s, a.B - 1);        // rows of absent samples only feed unstored outputs
-      aoff1[qq] = (b * G::LIN + li) * a.c1 + c * G::EPC;
-      aoff2[qq] = (b * G::LIN + li) * a.c2 + c * G::EPC;
+      avoff1[qq] = ((b * G::LIN + li) * a.c1 + c * G::EPC) * (int)sizeof(T);
+      avoff2[qq] = ((b * G::LIN + li) * a.c2 + c * G::EPC) * (int)sizeof(T);
     }
-    wbase = reinterpret_cast<const char*>(a.wpack) + (size_t)n_tile * NC * G::B_BYTES + (size_t)(wv * 64 + lane) * 16;
+    bvoff = (wv * 64 + lane) * 16;
+    wbase = n_tile * NC * G::B_BYTES;
   }
 
-  // issue DMA piece k (0..PER-1) of chunk kc into stage buf
-  __device__ __forceinline__ void piece(const ConvArgs<T>& a, char* smem, int k, int kc, int buf, int lane) const {
-    char* sbase = smem + buf * G::STAGE;
+  // issue DMA piece k (0..PER-1) of chunk kc into stage sbase
+  __device__ __forceinline__ void piece(char* sbase, int k, int kc, int lane) const {
     if (k < G::APT) {
       const int p0 = k * kThreads + wv * 64;
       if (G::AFULL || p0 < G::APIECES) {
         if (G::AFULL || p0 + lane < G::APIECES) {
-          const T* g = kc < n1 ? a.src1 + aoff1[k] + kc * G::KC : a.src2 + aoff2[k] + (kc - n1) * G::KC;
-          __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(sbase + p0 * 16), 16, 0, 0);
+          const bool first = kc < n1;
+          const int soff = (first ? kc : kc - n1) * G::KC * (int)sizeof(T);
+          llvm_amdgcn_raw_buffer_load_lds(first ? rs1 : rs2, (__attribute__((address_space(3))) void*)(sbase + p0 * 16),
+                                          16, first ? avoff1[k] : avoff2[k], soff, 0, 0);
         }
       }
     } else {
       const int qq = k - G::APT;
       const int p0 = qq * kThreads + wv * 64;
-      __builtin_amdgcn_global_load_lds(wbase + (size_t)kc * G::B_BYTES + qq * kThreads * 16,
-                                       (__attribute__((address_space(3))) void*)(sbase + G::A_BYTES + p0 * 16), 16,
-                                       0, 0);
+      llvm_amdgcn_raw_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(sbase + G::A_BYTES + p0 * 16), 16,
+                                      bvoff + qq * kThreads * 16, wbase + kc * G::B_BYTES, 0, 0);
     }
   }
 
-  __device__ __forceinline__ void all(const ConvArgs<T>& a, char* smem, int kc, int buf, int lane) const {
+  __device__ __forceinline__ void all(char* smem, int kc, int buf, int lane) const {
 #pragma unroll
-    for (int k = 0; k < G::PER; ++k) piece(a, smem, k, kc, buf, lane);
+    for (int k = 0; k < G::PER; ++k) piece(smem + buf * G::STAGE, k, kc, lane);
   }
 };
 
@@ -337,10 +363,13 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
   dma.init(a, m0, n_tile, NC, wv, lane);
 
   // One chunk: TAPS x (ROWB/32 bf16 | ROWB/64 f32) MFMA steps.  The DMA pieces of
-  // chunk nkc (into stage nbuf) are issued spread over the steps (nkc < 0: none).
-  auto compute = [&](const char* base, int nkc, int nbuf) {
+  // chunk nkc (into stage nbuf) are issued spread over the steps (NEXT = false: none).
+  // sched_barriers pin the order per step: [LDS reads of step s | DMA pieces] then
+  // [MFMAs of step s-1], so every read has one MFMA group (6 x 32 cycles) to land.
+  auto compute = [&](const char* base, auto next_tag, int nkc, int nbuf) {
+    constexpr bool NEXT = decltype(next_tag)::value;
+    char* nbase = smem + nbuf * G::STAGE;
     if constexpr (sizeof(T) == 2) {
-      // step = (tap j, 16-k group g); fragments of step+1 are read while step's MFMAs run
       constexpr int NG = ROWB / 32;
       constexpr int NS = TAPS * NG;
       constexpr int PPS = (G::PER + NS - 1) / NS;   // DMA pieces per step
@@ -355,11 +384,12 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
           for (int jn = 0; jn < 2; ++jn)
             bv[sb][jn] = *reinterpret_cast<const bf16x8*>(base + ((boff[jn] + j * NT * ROWB) ^ (g << 5)));
         }
-        if (nkc >= 0) {
+        if constexpr (NEXT) {
 #pragma unroll
           for (int u = 0; u < PPS; ++u)
-            if (st * PPS + u < G::PER) dma.piece(a, smem, st * PPS + u, nkc, nbuf, lane);
+            if (st * PPS + u < G::PER) dma.piece(nbase, st * PPS + u, nkc, lane);
         }
+        __builtin_amdgcn_sched_barrier(0);
         if (st > 0) {
           const int pb = (st - 1) & 1;
 #pragma unroll
@@ -368,6 +398,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
             for (int jn = 0; jn < 2; ++jn)
               acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[pb][i], bv[pb][jn], acc[i][jn], 0, 0, 0);
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
     } else {
       constexpr int NG = ROWB / 64;
@@ -388,11 +419,11 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
             bv0[jn] = *reinterpret_cast<const f32x4*>(base + ((boff[jn] + j * NT * ROWB) ^ (g << 6)));
             bv1[jn] = *reinterpret_cast<const f32x4*>(base + ((boff[jn] + j * NT * ROWB) ^ (g << 6) ^ 16));
           }
-          if (nkc >= 0) {
+          if constexpr (NEXT) {
             const int st = j * NG + g;
 #pragma unroll
             for (int u = 0; u < PPS; ++u)
-              if (st * PPS + u < G::PER) dma.piece(a, smem, st * PPS + u, nkc, nbuf, lane);
+              if (st * PPS + u < G::PER) dma.piece(nbase, st * PPS + u, nkc, lane);
           }
 #pragma unroll
           for (int s4 = 0; s4 < 4; ++s4)
@@ -412,35 +443,45 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
       }
     }
   };
+  using Yes = std::integral_constant<bool, true>;
+  using No = std::integral_constant<bool, false>;
 
   if constexpr (G::STAGES == 2) {
-    dma.all(a, smem, 0, 0, lane);
+    dma.all(smem, 0, 0, lane);
     wait_vmcnt<0>();
     __syncthreads();
-    for (int kc = 0; kc < NC; ++kc) {
-      compute(smem + (kc & 1) * G::STAGE, kc + 1 < NC ? kc + 1 : -1, (kc + 1) & 1);
+    for (int kc = 0; kc + 1 < NC; ++kc) {
+      compute(smem + (kc & 1) * G::STAGE, Yes{}, kc + 1, (kc + 1) & 1);
       wait_vmcnt<0>();
       __syncthreads();
     }
+    compute(smem + ((NC - 1) & 1) * G::STAGE, No{}, 0, 0);
+    __syncthreads();
   } else {
     // 3-deep ring: chunk kc+2 is in flight while chunk kc is computed; the wait
     // before each barrier retires chunk kc+1 only (counted vmcnt, never 0 mid-loop).
-    dma.all(a, smem, 0, 0, lane);
+    dma.all(smem, 0, 0, lane);
     if (NC > 1) {
-      dma.all(a, smem, 1, 1, lane);
+      dma.all(smem, 1, 1, lane);
       ring_barrier<G::PER>();
     } else {
       ring_barrier<0>();
     }
     int buf = 0;
-    for (int kc = 0; kc < NC; ++kc) {
+    for (int kc = 0; kc + 2 < NC; ++kc) {
       const int nb = buf == 0 ? 2 : buf - 1;          // (kc + 2) % 3
-      const bool more = kc + 2 < NC;
-      compute(smem + buf * G::STAGE, more ? kc + 2 : -1, nb);
-      if (more) ring_barrier<G::PER>();
-      else ring_barrier<0>();
+      compute(smem + buf * G::STAGE, Yes{}, kc + 2, nb);
+      ring_barrier<G::PER>();
       buf = buf == 2 ? 0 : buf + 1;
     }
+    // tail: the last (up to) two chunks, nothing left to prefetch
+    if (NC >= 2) {
+      compute(smem + buf * G::STAGE, No{}, 0, 0);
+      ring_barrier<0>();
+      buf = buf == 2 ? 0 : buf + 1;
+    }
+    compute(smem + buf * G::STAGE, No{}, 0, 0);
+    ring_barrier<0>();
   }
 
   // ------------------------------- epilogue --------------------------------
