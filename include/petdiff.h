@@ -152,6 +152,14 @@ int petdiff_generate(petdiff_handle h, const float* x_T_dev, const int32_t* tac_
                      uint64_t sample_offset, float* x_out_dev, float* all_xt_dev, int B, int use_graph,
                      void* stream);
 
+/* Fills out_dev [B][n_roi][n_par] with N(0,1) from the sampler's counter-based
+ * Philox stream (sample g = sample_offset + b, step id rng_step; the reverse loop
+ * uses step ids 0..n_steps-1, so x_T conventionally uses 0x7fffffff).  Replaces the
+ * caller's tf.random.normal x_T draw (main_script.py:415) when a world-size
+ * independent sharded run is wanted. */
+int petdiff_philox_normal(petdiff_handle h, uint64_t seed, uint64_t sample_offset, int rng_step, float* out_dev,
+                          int B, void* stream);
+
 /* Per (condition, roi, param) {count, mean, M2} in fp64 over the samples of
  * x0_dev [B][n_roi][n_par] (host output [n_tac][n_roi][n_par][3]; synchronises
  * the stream).  mean / sqrt(M2 / count) = main_script.py:433-436. */

@@ -50,6 +50,8 @@ SYMBOLS = [
                                    C.c_void_p]),
     ('petdiff_posterior_stats', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
                                           C.c_void_p]),
+    ('petdiff_philox_normal', C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_int, C.c_void_p, C.c_int,
+                                        C.c_void_p]),
     ('petdiff_set_timing', C.c_int, [C.c_void_p, C.c_int]),
     ('petdiff_get_timing', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ('petdiff_last_error', C.c_char_p, []),

@@ -702,6 +702,14 @@ int petdiff_generate(petdiff_handle h, const float* x_T, const int32_t* tac, con
   return PETDIFF_OK;
 }
 
+int petdiff_philox_normal(petdiff_handle h, uint64_t seed, uint64_t sample_offset, int rng_step, float* out, int B,
+                          void* stream) {
+  CHK(valid_handle(h));
+  if (B < 0 || (B > 0 && !out)) return fail(PETDIFF_ERR_INVALID, "bad arguments");
+  HIPC(launch_philox_normal(seed, sample_offset, rng_step, B, out, (hipStream_t)stream));
+  return PETDIFF_OK;
+}
+
 int petdiff_posterior_stats(petdiff_handle h, const float* x0, const int32_t* tac, int B, int n_tac,
                             double* stats, void* stream) {
   CHK(valid_handle(h));

@@ -89,6 +89,8 @@ hipError_t launch_dense(const float* in, int rows, int din, const float* w, cons
 hipError_t launch_fold(const float* seq, int n, int Lseq, int Cs, const float* wk, int taps, int padl,
                        int ups, int cin_full, int ch0, const float* wr, const float* b1,
                        const float* b2, float* out, int Lout, int cout, hipStream_t s);
+hipError_t launch_philox_normal(unsigned long long seed, unsigned long long goff, int step, int B, float* out,
+                                hipStream_t s);
 hipError_t launch_posterior_stats(const float* x0, const int* tac, int B, int n_tac, int ncol,
                                   double* stats, hipStream_t s);
 

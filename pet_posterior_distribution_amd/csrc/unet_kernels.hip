@@ -748,6 +748,18 @@ __global__ void fold_map_kernel(const float* seq, int n, int Lseq, int Cs, const
   out[idx] = acc;
 }
 
+// x_T ~ N(0, 1) from the same counter-based stream (step id = rng_step), so a
+// sharded run draws exactly the samples of the unsharded one.
+__global__ void philox_normal_kernel(unsigned long long seed, unsigned long long goff, int step, int B, float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // (sample, roi)
+  if (i >= B * 48) return;
+  const int b = i / 48, roi = i - b * 48;
+  float z[2];
+  philox_normal2(seed, goff + (unsigned long long)b, step, roi, z);
+  out[(size_t)i * 2] = z[0];
+  out[(size_t)i * 2 + 1] = z[1];
+}
+
 // Per (TAC, column) count / mean / M2 in fp64 (main_script.py:433-436 summary).
 __global__ void posterior_stats_kernel(const float* x0, const int* tac, int B, int ncol, double* stats) {
   __shared__ double red[256];
@@ -853,6 +865,13 @@ hipError_t launch_fold(const float* seq, int n, int Lseq, int Cs, const float* w
   if (tot == 0) return hipSuccess;
   hipLaunchKernelGGL(fold_map_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, seq, n, Lseq, Cs, wk,
                      taps, padl, ups, cin_full, ch0, wr, b1, b2, out, Lout, cout);
+  return hipGetLastError();
+}
+
+hipError_t launch_philox_normal(unsigned long long seed, unsigned long long goff, int step, int B, float* out,
+                                hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  hipLaunchKernelGGL(philox_normal_kernel, dim3((B * 48 + 255) / 256), dim3(256), 0, s, seed, goff, step, B, out);
   return hipGetLastError();
 }
 

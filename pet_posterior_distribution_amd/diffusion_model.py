@@ -182,11 +182,13 @@ class ImprovedDDPM:
         except Exception:
             pass
 
-    def _conditions(self, condition, B):
+    def _conditions(self, condition, B, tac=None):
         """Deduplicate conditions -> (per-sample index tensor or None).
 
         The reference feeds np.repeat(y_obs, B) (main_script.py:419); the kernels
         fold each UNIQUE condition once (encoder + label maps) and index it per sample.
+        With ``tac`` given, ``condition`` is the (n_tac, 49, 54) table and tac[b] the
+        row of sample b (no deduplication).
         """
         h = self._ensure_handle()
         if condition is None:
@@ -196,9 +198,16 @@ class ImprovedDDPM:
             cond = cond[None]
         if cond.shape[1:] != (49, 54):
             raise ValueError(f'condition must be (B, 49, 54), got {tuple(cond.shape)}')
-        if cond.shape[0] != B and cond.shape[0] != 1:
+        if tac is not None:
+            inv = _as_device(tac, self.device, torch.int32).reshape(-1)
+            if inv.numel() != B:
+                raise ValueError('tac must have one entry per sample')
+            if B and (int(inv.min()) < 0 or int(inv.max()) >= cond.shape[0]):
+                raise ValueError('tac index out of range')
+            uniq = cond.contiguous()
+        elif cond.shape[0] != B and cond.shape[0] != 1:
             raise ValueError(f'condition batch {cond.shape[0]} != x batch {B}')
-        if cond.shape[0] == 1 or bool((cond == cond[:1]).all()):
+        elif cond.shape[0] == 1 or bool((cond == cond[:1]).all()):
             uniq, inv = cond[:1].contiguous(), None
         else:
             uniq, inv = torch.unique(cond.reshape(cond.shape[0], -1), dim=0, return_inverse=True)
@@ -274,18 +283,18 @@ class ImprovedDDPM:
         raise ValueError('Subsequence type not recognized (given {})'.format(sub_sequence_type))
 
     def ddpm_loop(self, x_T, condition, num_timesteps=None, sub_sequence_type='linear', flag_var_tilde=True,
-                  keep_all_xt=False, z=None, seed=None, sample_offset=0, use_graph=True):
+                  keep_all_xt=False, z=None, seed=None, sample_offset=0, use_graph=True, tac=None):
         """ImprovedDDPM.ddpm_loop = generate (diffusion_model.py:670-715).
 
         Extra keywords: ``z`` injected noise (n_steps, B, 48, 2); ``seed`` /
         ``sample_offset`` select the counter-based noise stream (global index of
         sample b is sample_offset + b); ``use_graph`` replays the whole loop as one
-        captured hipGraph.
+        captured hipGraph; ``tac`` indexes a (n_tac, 49, 54) condition table per sample.
         """
         indices = self.sub_sequence(num_timesteps, sub_sequence_type)
         x = _as_device(x_T, self.device, torch.float32)
         B = x.shape[0]
-        tac, _ = self._conditions(condition, B)
+        tac, _ = self._conditions(condition, B, tac)
         n = len(indices)
         zt = None if z is None else _as_device(z, self.device, torch.float32)
         if zt is not None and tuple(zt.shape) != (n,) + tuple(x.shape):
@@ -310,6 +319,16 @@ class ImprovedDDPM:
     def tfunc_ddpm_loop(self, x_T, condition, **kwargs):
         """diffusion_model.py:718-737: full-T loop, var_tilde, one captured graph."""
         return self.ddpm_loop(x_T, condition, num_timesteps=None, flag_var_tilde=True, use_graph=True, **kwargs)
+
+    def philox_normal(self, B, seed=None, sample_offset=0, rng_step=0x7fffffff):
+        """x_T ~ N(0,1) (B, 48, 2) from the counter-based stream: sample b is global sample
+        sample_offset + b, so shards of one run reproduce the unsharded draw exactly."""
+        h = self._ensure_handle()
+        out = torch.empty((B, 48, 2), dtype=torch.float32, device=self.device)
+        _lib.check(_lib.lib().petdiff_philox_normal(h, self.seed if seed is None else int(seed), int(sample_offset),
+                                                    int(rng_step), _ptr(out), B, _stream_ptr(self.device)),
+                   'petdiff_philox_normal')
+        return out
 
     # ---------------------------------------------------------- summaries
     def posterior_stats(self, x0, tac=None, n_tac=1):

@@ -1,0 +1,107 @@
+"""Multi-GPU sharding of posterior sampling.
+
+Posterior samples and test TACs are independent units: every rank (one process
+per GPU, torch.distributed over RCCL) samples a contiguous block of the global
+(TAC, sample) index space with no per-step communication.  The noise of global
+sample g is Philox(seed, g, step), so the result is independent of the world
+size.  The only collective is one all-gather of per-(TAC, ROI, parameter)
+Welford partials {count, mean, M2} (fp64, 2,304 B per TAC), merged with Chan's
+parallel formula into the population mean / std of main_script.py:433-436.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def shard_range(n_total, world, rank):
+    """Contiguous block [lo, hi) of n_total units owned by `rank` (sizes differ by <= 1)."""
+    base, rem = divmod(n_total, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def tac_major_shards(n_tac, n_per_tac, world, rank):
+    """Global sample indices of `rank` for n_tac TACs x n_per_tac samples, TAC-major
+    (whole TACs per rank when n_tac >= world).  Returns (lo, hi) over g = tac*n_per_tac + s."""
+    return shard_range(n_tac * n_per_tac, world, rank)
+
+
+def merge_stats(parts):
+    """Chan et al. pairwise merge of [..., 3] {count, mean, M2} partials along axis 0."""
+    parts = np.asarray(parts, dtype=np.float64)
+    n, mean, m2 = parts[0, ..., 0].copy(), parts[0, ..., 1].copy(), parts[0, ..., 2].copy()
+    for p in parts[1:]:
+        nb, mb, m2b = p[..., 0], p[..., 1], p[..., 2]
+        tot = n + nb
+        with np.errstate(invalid='ignore', divide='ignore'):
+            delta = mb - mean
+            w = np.where(tot > 0, nb / np.where(tot > 0, tot, 1), 0.0)
+            mean = mean + delta * w
+            m2 = m2 + m2b + delta * delta * np.where(tot > 0, n * nb / np.where(tot > 0, tot, 1), 0.0)
+        n = tot
+    return np.stack([n, mean, m2], axis=-1)
+
+
+def local_stats_numpy(x, tac=None, n_tac=1):
+    """Reference {count, mean, M2} of samples x (B, 48, 2) per condition (host, for tests)."""
+    x = np.asarray(x, dtype=np.float64)
+    tac = np.zeros(x.shape[0], dtype=np.int64) if tac is None else np.asarray(tac)
+    out = np.zeros((n_tac,) + x.shape[1:] + (3,))
+    for k in range(n_tac):
+        xs = x[tac == k]
+        if xs.shape[0]:
+            out[k, ..., 0] = xs.shape[0]
+            out[k, ..., 1] = xs.mean(0)
+            out[k, ..., 2] = ((xs - xs.mean(0)) ** 2).sum(0)
+    return out
+
+
+def allgather_stats(stats, group=None, device=None):
+    """All-gather this rank's [n_tac_local, ...,3] partials; returns [world, ...] on the host.
+
+    Uses the process group's backend (nccl = RCCL over xGMI on MI355X, gloo on CPU)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.as_tensor(np.ascontiguousarray(stats), dtype=torch.float64)
+    if device is not None:
+        t = t.to(device)
+    world = dist.get_world_size(group)
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t, group=group)
+    return np.stack([o.cpu().numpy() for o in out])
+
+
+def summarize(stats):
+    """{count, mean, M2} -> mean / population std (ddof=0) per ROI for DVR (ch 0) and R1 (ch 1)."""
+    cnt, mean, m2 = stats[..., 0], stats[..., 1], stats[..., 2]
+    std = np.sqrt(m2 / np.maximum(cnt, 1))
+    return {'mean_DVR': mean[..., 0], 'mean_R1': mean[..., 1], 'std_DVR': std[..., 0], 'std_R1': std[..., 1]}
+
+
+def sample_posterior_sharded(model, cond_all, n_per_tac, seed=0, x_T_seed=1, group=None, use_graph=True):
+    """Config 4 driver: n_tac TACs x n_per_tac samples sharded TAC-major over the ranks.
+
+    Each rank generates its block (x_T and z from counter-based Philox keyed by the
+    global sample index, so the result does not depend on the world size), reduces it on the GPU to per-TAC Welford partials, and the
+    partials are all-gathered (RCCL) and merged.  Returns per-TAC summary dicts."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    n_tac = cond_all.shape[0]
+    lo, hi = tac_major_shards(n_tac, n_per_tac, world, rank)
+    stats = np.zeros((n_tac, 48, 2, 3))
+    if hi > lo:
+        g = np.arange(lo, hi)
+        tac_g = g // n_per_tac
+        tacs = np.unique(tac_g)
+        cond = np.asarray(cond_all)[tacs]
+        local_tac = np.searchsorted(tacs, tac_g).astype(np.int32)
+        x_T = model.philox_normal(hi - lo, seed=x_T_seed, sample_offset=lo)
+        x0 = model.ddpm_loop(x_T, cond, seed=seed, sample_offset=lo, use_graph=use_graph, tac=local_tac)
+        st = model.posterior_stats(x0, local_tac, n_tac=len(tacs))
+        stats[tacs] = st
+    if world > 1:
+        parts = allgather_stats(stats, group=group, device=model.device)
+        stats = merge_stats(parts)
+    return summarize(stats), stats

@@ -1,0 +1,290 @@
+"""CPU tests: the oracle against the reference's golden vectors, the host logic of the
+product (schedule tables, sub-sequences, weight spec, synthetic data), and the
+multi-rank statistics merge over gloo (world_size 2)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import iddpm_ref as R
+from oracle import srtm2_ref as K
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+
+
+# ---------------------------------------------------------------- G1: schedules
+def test_oracle_schedules_bitexact_vs_reference():
+    g = np.load(os.path.join(GOLD, 'g1_schedules.npz'))
+    np.testing.assert_array_equal(R.get_beta_schedule('cosine', 1000), g['cosine_T1000'])
+    np.testing.assert_array_equal(R.get_beta_schedule('cosine', 200), g['cosine_T200'])
+    np.testing.assert_array_equal(R.get_beta_schedule('linear', 1000), g['linear_T1000'])
+    np.testing.assert_array_equal(R.get_beta_schedule('quadratic', 1000), g['quadratic_T1000'])
+    np.testing.assert_array_equal(R.get_beta_schedule('sigmoid', 1000), g['sigmoid_T1000'])
+
+
+def test_product_schedules_bitexact_vs_reference():
+    from pet_posterior_distribution_amd import helper_func as hf
+    g = np.load(os.path.join(GOLD, 'g1_schedules.npz'))
+    kw = dict(beta_start=1e-4, beta_end=2e-2, offset_s=0.008, max_beta=0.999)
+    for name, key in [('cosine', 'cosine_T1000'), ('linear', 'linear_T1000'), ('quadratic', 'quadratic_T1000'),
+                      ('sigmoid', 'sigmoid_T1000')]:
+        np.testing.assert_array_equal(hf.get_beta_schedule(name, 1000, **kw), g[key])
+    with pytest.raises(NotImplementedError):
+        hf.get_beta_schedule('exp', 10)
+
+
+def test_schedule_known_values():
+    """Survey a1 known answers (beta_0, beta_999, alpha_bar_999, plvc[0] == plvc[1])."""
+    S = R.schedule_tables(R.get_beta_schedule('cosine', 1000))
+    assert abs(S['beta'][0] - 4.1246e-5) < 1e-8
+    assert S['beta'][-1] == np.float32(0.999)
+    assert abs(S['alpha_bar'][-1] - 2.4289e-9) < 1e-12
+    assert S['posterior_log_variance_clipped'][0] == S['posterior_log_variance_clipped'][1]
+    assert abs(S['posterior_log_variance_clipped'][0] + 10.734668) < 1e-5
+    assert S['posterior_variance'][0] == S['posterior_variance'][1]      # the alias quirk (:349-351)
+
+
+def test_product_tables_match_oracle():
+    """ImprovedDDPM's host tables (handed to libpetdiff) == the oracle's restatement."""
+    from pet_posterior_distribution_amd import ImprovedDDPM, UnetConditional
+    from pet_posterior_distribution_amd.configs import shipped_net_args, shipped_diff_args
+    m = ImprovedDDPM(network=UnetConditional(**shipped_net_args()), **shipped_diff_args())
+    S = R.schedule_tables(R.get_beta_schedule('cosine', 1000))
+    tab = m.schedule_tables()
+    assert tab.shape == (13, 1000) and tab.dtype == np.float32
+    np.testing.assert_array_equal(tab[0], S['beta'])
+    np.testing.assert_array_equal(tab[2], S['posterior_log_variance_clipped'])
+    np.testing.assert_array_equal(tab[4], S['posterior_mean_coef1'])
+    np.testing.assert_array_equal(tab[5], S['posterior_mean_coef2'])
+    np.testing.assert_array_equal(tab[6], S['alpha_bar'])
+    np.testing.assert_array_equal(tab[9], np.float32(1) / S['sqrt_alpha_bar'])
+
+
+def test_improved_ddpm_errors_match_reference():
+    from pet_posterior_distribution_amd import ImprovedDDPM, UnetConditional
+    from pet_posterior_distribution_amd.configs import shipped_net_args, shipped_diff_args
+    with pytest.raises(ValueError, match='Input network is required'):
+        ImprovedDDPM(network=None, **shipped_diff_args())
+    with pytest.raises(ValueError, match='Invalid parameterization'):
+        ImprovedDDPM(network=UnetConditional(**shipped_net_args()), parameterization='foo', **shipped_diff_args())
+    m = ImprovedDDPM(network=UnetConditional(**shipped_net_args()), **shipped_diff_args())
+    with pytest.raises(ValueError, match='Subsequence type not recognized'):
+        m.sub_sequence(10, 'cubic')
+
+
+# ---------------------------------------------------------------- sub-sequences
+def test_loop_indices_reference_semantics():
+    assert R.loop_indices(1000) == list(range(1000))[::-1]
+    lin = R.loop_indices(1000, 100, 'linear')
+    assert lin[:5] == [999, 988, 978, 968, 958] and lin[-1] == 0 and len(lin) == 100
+    quad = R.loop_indices(1000, 100, 'quadratic')
+    assert quad[:3] == [961, 961, 900] and len(set(quad)) == 32          # survey hard-part (a)
+    assert R.loop_indices(1000, 10, 'lin') == R.loop_indices(1000, 10, 'linear')   # substring test :683
+    from pet_posterior_distribution_amd import ImprovedDDPM, UnetConditional
+    from pet_posterior_distribution_amd.configs import shipped_net_args, shipped_diff_args
+    m = ImprovedDDPM(network=UnetConditional(**shipped_net_args()), **shipped_diff_args())
+    for n, kind in [(None, 'linear'), (100, 'linear'), (100, 'quadratic'), (1000, 'quadratic'), (7, 'l')]:
+        assert m.sub_sequence(n, kind) == R.loop_indices(1000, n, kind)
+
+
+# ---------------------------------------------------------------- network spec
+def test_param_spec_structure():
+    from pet_posterior_distribution_amd.networks import param_spec
+    spec = param_spec()
+    assert spec == R.param_spec()
+    assert sum(int(np.prod(s)) for _, s in spec) == 11_851_740
+    d = dict(spec)
+    assert d['down0.conv.kernel'] == (6, 52, 128) and d['down3.conv.kernel'] == (6, 562, 1024)
+    assert d['up0.upconv.kernel'] == (2, 1074, 512) and d['up2.conv.kernel'] == (6, 256, 128)
+    assert d['final.kernel'] == (1, 128, 4)
+
+
+def test_unsupported_configs_raise():
+    from pet_posterior_distribution_amd import UnetConditional
+    from pet_posterior_distribution_amd.configs import shipped_net_args
+    a = shipped_net_args()
+    a['depth'] = 5
+    with pytest.raises(NotImplementedError):
+        UnetConditional(**a)
+    a = shipped_net_args()
+    a['block_params'] = {'flag_res': True, 'kernel_size': 6, 'norm_list': 'pre'}
+    with pytest.raises(NotImplementedError):
+        UnetConditional(**a)
+
+
+def test_denoiser_init_identity_path_and_bounded_chain():
+    """The synthetic weights predict eps ~ x (+ small perturbation); a short chain stays finite."""
+    from pet_posterior_distribution_amd.networks import denoiser_init, param_spec
+    P = denoiser_init(param_spec(), seed=3)
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((2, 48, 2))
+    cond = np.abs(rng.standard_normal((2, 49, 54)))
+    out = R.unet_forward(P, x, np.array([999, 10]), cond)
+    assert np.abs(out[..., :2] - x).max() < 1.0
+    S = R.schedule_tables(R.get_beta_schedule('cosine', 1000))
+    idx = R.loop_indices(1000, 10)
+    x0 = R.ddpm_loop(P, S, x, cond[:1], rng.standard_normal((10, 2, 48, 2)), idx, dt=np.float64)
+    assert np.isfinite(x0).all()
+
+
+def test_oracle_keras_semantics():
+    """conv1d_same padding (TF SAME: left (k-1)//2), raw reshape, maxpool / upsample."""
+    x = np.arange(1, 7, dtype=np.float64).reshape(1, 6, 1)
+    W = np.zeros((6, 1, 1))
+    W[0] = 1.0                               # tap 0 reads position l - 2
+    np.testing.assert_array_equal(R.conv1d_same(x, W, 0.0)[0, :, 0], [0, 0, 1, 2, 3, 4])
+    W = np.zeros((2, 1, 1))
+    W[1] = 1.0                               # k=2: pad right 1 -> tap 1 reads l + 1
+    np.testing.assert_array_equal(R.conv1d_same(x, W, 0.0)[0, :, 0], [2, 3, 4, 5, 6, 0])
+    np.testing.assert_array_equal(R.maxpool2(x)[0, :, 0], [2, 4, 6])
+    np.testing.assert_array_equal(R.upsample2(x)[0, :4, 0], [1, 1, 2, 2])
+
+
+def test_oracle_fp32_close_to_fp64():
+    from pet_posterior_distribution_amd.networks import denoiser_init, param_spec
+    P = denoiser_init(param_spec(), seed=5, bias_scale=0.05)
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((2, 48, 2))
+    cond = np.abs(rng.standard_normal((2, 49, 54)))
+    a = R.unet_forward(P, x, np.array([500, 3]), cond, dt=np.float64)
+    b = R.unet_forward(P, x, np.array([500, 3]), cond, dt=np.float32)
+    assert np.abs(a - b).max() / np.abs(a).max() < 1e-5
+
+
+# ---------------------------------------------------------------- Philox
+def test_philox_known_answers():
+    """Random123 philox4x32-10 known-answer vectors."""
+    out = R.philox4x32_10(0, 0, 0, 0, 0, 0)
+    assert [int(v) for v in out] == [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]
+    f = 0xffffffff
+    out = R.philox4x32_10(f, f, f, f, f, f)
+    assert [int(v) for v in out] == [0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd]
+    out = R.philox4x32_10(0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344, 0xa4093822, 0x299f31d0)
+    assert [int(v) for v in out] == [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]
+
+
+def test_philox_normals_statistics():
+    z = R.philox_normal_pairs(12345, np.arange(4000), 3)
+    assert z.shape == (4000, 48, 2)
+    assert abs(z.mean()) < 0.01 and abs(z.std() - 1) < 0.01
+
+
+# ---------------------------------------------------------------- G2: SRTM2
+def test_srtm2_oracle_vs_reference_golden():
+    g = np.load(os.path.join(GOLD, 'g2_srtm2.npz'))
+    tv = g['time_vector']
+    for k in range(4):
+        tac = K.srtm2_tac(tv, g[f'case{k}_tac_ref'], g[f'case{k}_DVR'], g[f'case{k}_R1'], float(g[f'case{k}_k2p']))
+        np.testing.assert_allclose(tac, g[f'case{k}_tac'], rtol=1e-12, atol=1e-14)
+    up = K.interp1d_linear_vec(g['interp_x'], tv, np.exp(-0.05 * tv)[:, None] * np.arange(1, 4)[None, :])
+    np.testing.assert_allclose(up, g['interp_up'], rtol=1e-13, atol=1e-15)
+
+
+def test_srtm2_operator_reassociation():
+    """TAC = R1 C_r + (k2 - R1 k2a) M exp(-k2a t) with the constant 54x54 M (used by the MH kernel)."""
+    g = np.load(os.path.join(GOLD, 'g2_srtm2.npz'))
+    tv = g['time_vector']
+    M = K.srtm2_operator(tv, g['case0_tac_ref'])
+    DVR, R1, k2p = g['case0_DVR'], g['case0_R1'], float(g['case0_k2p'])
+    k2 = k2p * R1
+    k2a = k2 / DVR
+    e = np.exp(-k2a[None, :] * tv[:, None])
+    tac = R1 * g['case0_tac_ref'][:, None] + (k2 - R1 * k2a) * (M @ e)
+    np.testing.assert_allclose(tac, g['case0_tac'], rtol=1e-11, atol=1e-13)
+
+
+def test_product_srtm2_host_vs_reference_golden():
+    from pet_posterior_distribution_amd.sim_data import srtm2_tac, time_grid
+    g = np.load(os.path.join(GOLD, 'g2_srtm2.npz'))
+    tv, dt = time_grid()
+    np.testing.assert_array_equal(tv, g['time_vector'])
+    np.testing.assert_array_equal(dt, g['dt'])
+    for k in range(4):
+        tac = srtm2_tac(g[f'case{k}_DVR'], g[f'case{k}_R1'], float(g[f'case{k}_k2p']), g[f'case{k}_tac_ref'], tv)
+        np.testing.assert_allclose(tac, g[f'case{k}_tac'], rtol=1e-12, atol=1e-14)
+
+
+def test_mh_log_posterior_and_sampler_smoke():
+    g = np.load(os.path.join(GOLD, 'g2_srtm2.npz'))
+    tv = g['time_vector']
+    ref = g['case0_tac_ref']
+    mu_D, mu_R = g['case0_DVR'], g['case0_R1']
+    cov_D = np.diag((0.1 * mu_D) ** 2)
+    cov_R = np.diag((0.1 * mu_R) ** 2)
+    sn = g['case0_tac'].T
+    sig = np.full_like(sn, 0.1)
+    y = sn + np.sqrt(sn) * 0.05
+    lp = K.log_posterior(mu_D, mu_R, float(g['case0_k2p']), y, sig, tv, ref, mu_D, cov_D, mu_R, cov_R)
+    assert np.isfinite(lp)
+    # tune table (pymc 5.12)
+    np.testing.assert_allclose(K.pymc_tune(np.ones(7), np.array([0.0005, 0.01, 0.1, 0.3, 0.6, 0.8, 0.99])),
+                               [0.1, 0.5, 0.9, 1.0, 1.1, 2.0, 10.0])
+
+
+# ---------------------------------------------------------------- synthetic data
+def test_acquisition_protocol():
+    from pet_posterior_distribution_amd.sim_data import acquisition_time_frames
+    f = acquisition_time_frames()
+    assert f.shape == (54, 2)
+    assert abs(f[0, 1] - 10 / 60) < 1e-12 and abs(f[-1, 1] - 120) < 1e-12
+    np.testing.assert_allclose(f[1:, 0], f[:-1, 1])
+
+
+def test_make_condition_shape():
+    from pet_posterior_distribution_amd.sim_data import make_condition
+    c = make_condition(3)
+    assert c.shape == (49, 54) and c.dtype == np.float32 and (c >= 0).all()
+
+
+# ---------------------------------------------------------------- distributed merge
+def test_merge_stats_matches_numpy():
+    from pet_posterior_distribution_amd.distributed import merge_stats, local_stats_numpy, summarize
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((1000, 48, 2)) * 2 + 3
+    parts = [local_stats_numpy(x[a:b]) for a, b in [(0, 100), (100, 601), (601, 1000)]]
+    st = merge_stats(parts)
+    s = summarize(st)
+    np.testing.assert_allclose(s['mean_DVR'][0], x[:, :, 0].mean(0), rtol=1e-12)
+    np.testing.assert_allclose(s['std_R1'][0], x[:, :, 1].std(0), rtol=1e-12)
+
+
+def test_shard_ranges_cover():
+    from pet_posterior_distribution_amd.distributed import shard_range
+    for n, w in [(10, 3), (8192 * 256, 8), (5, 8)]:
+        rs = [shard_range(n, w, r) for r in range(w)]
+        assert rs[0][0] == 0 and rs[-1][1] == n
+        assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
+
+
+def _gloo_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from pet_posterior_distribution_amd.distributed import (allgather_stats, merge_stats, local_stats_numpy,
+                                                           shard_range)
+    dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank, world_size=world)
+    rng = np.random.default_rng(42)
+    x = rng.standard_normal((777, 48, 2))
+    lo, hi = shard_range(777, world, rank)
+    parts = allgather_stats(local_stats_numpy(x[lo:hi]))
+    st = merge_stats(parts)
+    if rank == 0:
+        q.put((st[0, :, :, 1] - x.mean(0), np.sqrt(st[0, :, :, 2] / st[0, :, :, 0]) - x.std(0)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_allgather_merge():
+    import multiprocessing as mp
+    import socket
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    dm, ds = q.get(timeout=120)
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert np.abs(dm).max() < 1e-12 and np.abs(ds).max() < 1e-12
