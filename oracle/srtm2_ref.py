@@ -145,3 +145,42 @@ def metropolis_elemwise(logp, x0, n_draws, n_tune, rng, tune_interval=100, scali
         if it >= n_tune:
             out[it - n_tune] = x
     return out
+
+
+def philox_mh_noise(seed, chain, it, k):
+    """The GPU sampler's counter-based draws for element k of iteration `it` of `chain`:
+    Philox4x32-10(counter = (k, it, chain_lo, chain_hi), key = seed) -> N(0,1) proposal
+    (Box-Muller of words 0, 1) and the accept uniform (word 2)."""
+    from oracle.iddpm_ref import philox4x32_10
+    q = philox4x32_10(k, it, chain & 0xffffffff, chain >> 32, seed & 0xffffffff, (seed >> 32) & 0xffffffff)
+    u1 = (float(q[0]) + 1.0) * 2.0 ** -32
+    u2 = (float(q[1]) + 0.5) * 2.0 ** -32
+    ua = (float(q[2]) + 0.5) * 2.0 ** -32
+    return np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * u2), ua
+
+
+def metropolis_elemwise_philox(logp, x0, n_draws, n_tune, seed, chain, tune_interval=100, scaling=1.0):
+    """metropolis_elemwise with the GPU sampler's noise stream (identical chain path)."""
+    x = np.array(x0, dtype=np.float64)
+    lp = logp(x)
+    s = np.full(x.shape, float(scaling))
+    acc = np.zeros(x.shape)
+    kept_acc = np.zeros(x.shape)
+    out = np.empty((n_draws,) + x.shape)
+    for it in range(n_tune + n_draws):
+        if it < n_tune and it > 0 and it % tune_interval == 0:
+            s = pymc_tune(s, acc / tune_interval)
+            acc[:] = 0
+        for k in range(x.size):
+            z, ua = philox_mh_noise(seed, chain, it, k)
+            prop = x.copy()
+            prop[k] += z * s[k]
+            lpp = logp(prop)
+            if np.log(ua) < lpp - lp:
+                x, lp = prop, lpp
+                acc[k] += 1
+                if it >= n_tune:
+                    kept_acc[k] += 1
+        if it >= n_tune:
+            out[it - n_tune] = x
+    return out, kept_acc

@@ -56,7 +56,30 @@ SYMBOLS = [
     ('petdiff_get_timing', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ('petdiff_last_error', C.c_char_p, []),
     # Metropolis-Hastings / SRTM2 (include/petmh.h)
+    ('petmh_srtm2_tac', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
+                                  C.c_void_p, C.c_void_p]),
+    ('petmh_create', C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
+    ('petmh_destroy', C.c_int, [C.c_void_p]),
+    ('petmh_run', C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_p, C.c_void_p,
+                            C.c_void_p, C.c_void_p]),
+    ('petmh_logp', C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
+    ('petmh_last_error', C.c_char_p, []),
 ]
+
+
+class PetmhProblem(C.Structure):
+    _fields_ = [('n_roi', C.c_int), ('n_frames', C.c_int), ('time_vector', C.c_void_p), ('tac_ref', C.c_void_p),
+                ('k2p', C.c_double), ('y_obs', C.c_void_p), ('sigma_noise', C.c_void_p), ('mu_DVR', C.c_void_p),
+                ('cov_DVR', C.c_void_p), ('mu_R1', C.c_void_p), ('cov_R1', C.c_void_p)]
+
+
+def check_mh(rc, what=''):
+    if rc == 0:
+        return
+    msg = lib().petmh_last_error().decode(errors='replace')
+    if rc == 1:
+        raise ValueError(f'{what}: {msg}')
+    raise PetdiffError(f'{what}: {msg}')
 
 _lib = None
 

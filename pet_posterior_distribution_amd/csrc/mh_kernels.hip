@@ -1,0 +1,274 @@
+// CDNA4 kernels of the Metropolis-Hastings baseline (mcmc.py) and the SRTM2
+// forward model (kinetic_model.py), fp64 like the reference (mcmc.py:22).
+//
+// One 64-lane wavefront per chain.  Lane f (< 54) owns frame f of the TAC being
+// evaluated; lane r (< 48) owns ROI r of the chain state (DVR_r, R1_r, the prior
+// gradient g = P (x - mu) and the ROI log-likelihood).  An element-wise
+// Metropolis update of ROI i touches only ROI i's TAC (SRTM2 is per ROI), so a
+// proposal costs one 54 x 54 operator application + 54 truncated-normal terms;
+// the MvNormal prior change is 2 d g_i + d^2 P_ii (g kept current on accept).
+#include "mh_internal.h"
+
+namespace petmh {
+
+constexpr int NR = kNRoi, NF = kNFrames;
+constexpr int kWaves = 8;             // chains per workgroup (512 threads)
+
+struct Lds {
+  double M[NF * NF];                  // SRTM2 operator, [g][f]
+  double PD[NR * NR], PR[NR * NR];    // prior precision matrices
+  double Y[NR * NF], SIG[NR * NF];    // observed TAC / dt and noise sigma, [roi][frame]
+  double CR[NF], TV[NF];
+  double MUD[NR], MUR[NR];
+  double E[kWaves][64];               // per-wave exponential scratch
+};
+
+// Butterfly sum; lanes may differ in the last bit (different pairing order), so the
+// result is broadcast from lane 0 to keep every accept/reject decision wave-uniform.
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return __shfl(v, 0, 64);
+}
+
+__device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+    const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+}
+
+// log Phi(x) (scipy.special.log_ndtr), via erfc / erfcx for the left tail
+__device__ __forceinline__ double log_ndtr(double x) {
+  if (x > -1.0) return log(0.5 * erfc(-x * 0.7071067811865476));
+  return log(0.5 * erfcx(-x * 0.7071067811865476)) - 0.5 * x * x;
+}
+
+// Sum over frames of the TruncatedNormal(lower=0) log density of ROI i with
+// parameters (DVR, R1); every lane returns the total (mcmc.py:151-155).
+__device__ __forceinline__ double roi_loglik(const Lds& s, double* e, int lane, int i, double dvr, double r1, double k2p) {
+  const double k2 = k2p * r1;           // kinetic_model.py:153-154
+  const double k2a = k2 / dvr;
+  if (lane < NF) e[lane] = exp(-k2a * s.TV[lane]);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  double l = 0.0;
+  if (lane < NF) {
+    double conv = 0.0;
+#pragma unroll 6
+    for (int g = 0; g < NF; ++g) conv = fma(s.M[g * NF + lane], e[g], conv);
+    const double tac = r1 * s.CR[lane] + (k2 - r1 * k2a) * conv;   // :157-158
+    const double sn = tac < 0.0 ? 1e-6 : tac;                       // mcmc.py:152
+    const double sig = sqrt(sn) * s.SIG[i * NF + lane];             // :153
+    const double z = (s.Y[i * NF + lane] - sn) / sig;
+    l = -0.5 * z * z - 0.9189385332046727 - log(sig) - log_ndtr(sn / sig);
+  }
+  __builtin_amdgcn_wave_barrier();
+  return wave_sum(l);
+}
+
+__device__ void load_lds(Lds& s, const MHConst& c) {
+  for (int k = threadIdx.x; k < NF * NF; k += blockDim.x) s.M[k] = c.M[k];
+  for (int k = threadIdx.x; k < NR * NR; k += blockDim.x) { s.PD[k] = c.PD[k]; s.PR[k] = c.PR[k]; }
+  for (int k = threadIdx.x; k < NR * NF; k += blockDim.x) { s.Y[k] = c.Y[k]; s.SIG[k] = c.SIG[k]; }
+  for (int k = threadIdx.x; k < NF; k += blockDim.x) { s.CR[k] = c.CR[k]; s.TV[k] = c.TV[k]; }
+  for (int k = threadIdx.x; k < NR; k += blockDim.x) { s.MUD[k] = c.MUD[k]; s.MUR[k] = c.MUR[k]; }
+  __syncthreads();
+}
+
+__device__ __forceinline__ double tune_scale(double s, double rate) {   // pymc Metropolis tune()
+  if (rate < 0.001) return s * 0.1;
+  if (rate < 0.05) return s * 0.5;
+  if (rate < 0.2) return s * 0.9;
+  if (rate > 0.95) return s * 10.0;
+  if (rate > 0.75) return s * 2.0;
+  if (rate > 0.5) return s * 1.1;
+  return s;
+}
+
+__global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun r) {
+  __shared__ Lds s;
+  load_lds(s, c);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double* e = s.E[w];
+  const bool own = lane < NR;
+  const int li = own ? lane : 0;
+  for (int chain = blockIdx.x * kWaves + w; chain < r.n_chains; chain += gridDim.x * kWaves) {
+    // ---- state: lane l < 48 holds ROI l
+    double D = r.x0 ? r.x0[(size_t)chain * 2 * NR + li] : s.MUD[li];
+    double R = r.x0 ? r.x0[(size_t)chain * 2 * NR + NR + li] : s.MUR[li];
+    // prior gradients g = P (x - mu)
+    e[lane] = own ? D - s.MUD[lane] : 0.0;
+    __builtin_amdgcn_wave_barrier();
+    double gD = 0.0;
+#pragma unroll 1
+    for (int k = 0; k < NR; ++k) gD = fma(s.PD[li * NR + k], e[k], gD);
+    __builtin_amdgcn_wave_barrier();
+    e[lane] = own ? R - s.MUR[lane] : 0.0;
+    __builtin_amdgcn_wave_barrier();
+    double gR = 0.0;
+#pragma unroll 1
+    for (int k = 0; k < NR; ++k) gR = fma(s.PR[li * NR + k], e[k], gR);
+    __builtin_amdgcn_wave_barrier();
+    double ll = 0.0;
+#pragma unroll 1
+    for (int i = 0; i < NR; ++i) {
+      const double di = __shfl(D, i, 64), ri = __shfl(R, i, 64);
+      const double v = roi_loglik(s, e, lane, i, di, ri, c.k2p);
+      if (lane == i) ll = v;
+    }
+    double sD = r.scaling, sR = r.scaling;
+    int aD = 0, aR = 0;                  // accepts in the current tune window
+    double accD = 0.0, accR = 0.0;       // accepts over kept draws
+    double mD = 0.0, m2D = 0.0, mR = 0.0, m2R = 0.0;
+    long long nk = 0;
+    const int total = r.n_tune + r.n_draws;
+    for (int it = 0; it < total; ++it) {
+      if (it < r.n_tune && it > 0 && it % r.tune_interval == 0) {
+        sD = tune_scale(sD, (double)aD / r.tune_interval);
+        sR = tune_scale(sR, (double)aR / r.tune_interval);
+        aD = aR = 0;
+      }
+#pragma unroll 1
+      for (int v = 0; v < 2; ++v) {
+        const double* P = v == 0 ? s.PD : s.PR;
+#pragma unroll 1
+        for (int i = 0; i < NR; ++i) {
+          uint32_t q[4] = {(uint32_t)(v * NR + i), (uint32_t)it, (uint32_t)((unsigned long long)chain & 0xffffffffull),
+                           (uint32_t)((unsigned long long)chain >> 32)};
+          philox(q, (uint32_t)(r.seed & 0xffffffffull), (uint32_t)(r.seed >> 32));
+          const double u1 = ((double)q[0] + 1.0) * 2.3283064365386963e-10;
+          const double u2 = ((double)q[1] + 0.5) * 2.3283064365386963e-10;
+          const double ua = ((double)q[2] + 0.5) * 2.3283064365386963e-10;
+          const double zz = sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
+          const double xi = __shfl(v == 0 ? D : R, i, 64);
+          const double si = __shfl(v == 0 ? sD : sR, i, 64);
+          const double gi = __shfl(v == 0 ? gD : gR, i, 64);
+          const double lli = __shfl(ll, i, 64);
+          const double delta = zz * si;
+          const double xp = xi + delta;
+          const double dprior = -0.5 * (2.0 * delta * gi + delta * delta * P[i * NR + i]);
+          const double dn = v == 0 ? xp : __shfl(D, i, 64);
+          const double rn = v == 0 ? __shfl(R, i, 64) : xp;
+          const double lln = roi_loglik(s, e, lane, i, dn, rn, c.k2p);
+          const double logacc = dprior + lln - lli;
+          if (log(ua) < logacc) {          // wave-uniform decision
+            if (lane == i) {
+              if (v == 0) { D = xp; aD += 1; if (it >= r.n_tune) accD += 1.0; }
+              else { R = xp; aR += 1; if (it >= r.n_tune) accR += 1.0; }
+              ll = lln;
+            }
+            if (own) {
+              if (v == 0) gD = fma(delta, P[lane * NR + i], gD);
+              else gR = fma(delta, P[lane * NR + i], gR);
+            }
+          }
+        }
+      }
+      if (it >= r.n_tune) {              // Welford over kept draws
+        ++nk;
+        const double dd = D - mD;
+        mD += dd / (double)nk;
+        m2D = fma(dd, D - mD, m2D);
+        const double dr = R - mR;
+        mR += dr / (double)nk;
+        m2R = fma(dr, R - mR, m2R);
+      }
+    }
+    if (own) {
+      double* st = r.stats + (size_t)chain * 2 * NR * 3;
+      st[lane * 3 + 0] = (double)nk;
+      st[lane * 3 + 1] = mD;
+      st[lane * 3 + 2] = m2D;
+      st[(NR + lane) * 3 + 0] = (double)nk;
+      st[(NR + lane) * 3 + 1] = mR;
+      st[(NR + lane) * 3 + 2] = m2R;
+      if (r.accept) {
+        r.accept[(size_t)chain * 2 * NR + lane] = accD;
+        r.accept[(size_t)chain * 2 * NR + NR + lane] = accR;
+      }
+      if (r.last) {
+        r.last[(size_t)chain * 2 * NR + lane] = D;
+        r.last[(size_t)chain * 2 * NR + NR + lane] = R;
+      }
+    }
+  }
+}
+
+// Joint log density at n points (one wave per point).
+__global__ __launch_bounds__(kWaves * 64) void mh_logp_kernel(MHConst c, const double* x, int n, double* out) {
+  __shared__ Lds s;
+  load_lds(s, c);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double* e = s.E[w];
+  const int li = lane < NR ? lane : 0;
+  for (int pt = blockIdx.x * kWaves + w; pt < n; pt += gridDim.x * kWaves) {
+    const double D = x[(size_t)pt * 2 * NR + li], R = x[(size_t)pt * 2 * NR + NR + li];
+    double ll = 0.0;
+    for (int i = 0; i < NR; ++i) ll += roi_loglik(s, e, lane, i, __shfl(D, i, 64), __shfl(R, i, 64), c.k2p);
+    // MvNormal quadratic forms
+    double q = 0.0;
+    for (int v = 0; v < 2; ++v) {
+      const double* P = v == 0 ? s.PD : s.PR;
+      const double* mu = v == 0 ? s.MUD : s.MUR;
+      const double xv = v == 0 ? D : R;
+      e[lane] = lane < NR ? xv - mu[lane] : 0.0;
+      __builtin_amdgcn_wave_barrier();
+      double gi = 0.0;
+      if (lane < NR)
+        for (int k = 0; k < NR; ++k) gi = fma(P[lane * NR + k], e[k], gi);
+      q += wave_sum(lane < NR ? gi * e[lane] : 0.0);
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (lane == 0) out[pt] = ll - 0.5 * q + c.prior_const;
+  }
+}
+
+// Batched SRTM2 forward: one wave per (row, roi); tac [n][n_roi][NF].
+__global__ void srtm2_kernel(const double* M, const double* cr, const double* tv, const double* dvr,
+                             const double* r1, const double* k2p, int n, int n_roi, double* tac) {
+  __shared__ double e[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int item = blockIdx.x * 4 + w;
+  if (item >= n * n_roi) return;
+  const int row = item / n_roi;
+  const double R = r1[item], D = dvr[item];
+  const double k2 = k2p[row] * R, k2a = k2 / D;
+  if (lane < NF) e[w][lane] = exp(-k2a * tv[lane]);
+  __builtin_amdgcn_wave_barrier();
+  if (lane < NF) {
+    double conv = 0.0;
+    for (int g = 0; g < NF; ++g) conv = fma(M[g * NF + lane], e[w][g], conv);
+    tac[(size_t)item * NF + lane] = R * cr[lane] + (k2 - R * k2a) * conv;
+  }
+}
+
+hipError_t launch_mh_chains(const MHConst& c, const MHRun& r, hipStream_t st) {
+  if (r.n_chains <= 0) return hipSuccess;
+  int grid = (r.n_chains + kWaves - 1) / kWaves;
+  if (grid > 256 * 4) grid = 256 * 4;
+  hipLaunchKernelGGL(mh_chain_kernel, dim3(grid), dim3(kWaves * 64), 0, st, c, r);
+  return hipGetLastError();
+}
+
+hipError_t launch_mh_logp(const MHConst& c, const double* x, int n, double* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  int grid = (n + kWaves - 1) / kWaves;
+  if (grid > 1024) grid = 1024;
+  hipLaunchKernelGGL(mh_logp_kernel, dim3(grid), dim3(kWaves * 64), 0, st, c, x, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_srtm2(const double* M, const double* cr, const double* tv, const double* dvr, const double* r1,
+                        const double* k2p, int n, int n_roi, double* tac, hipStream_t st) {
+  const int items = n * n_roi;
+  if (items <= 0) return hipSuccess;
+  hipLaunchKernelGGL(srtm2_kernel, dim3((items + 3) / 4), dim3(256), 0, st, M, cr, tv, dvr, r1, k2p, n, n_roi, tac);
+  return hipGetLastError();
+}
+
+}  // namespace petmh
