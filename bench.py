@@ -44,18 +44,37 @@ def parse():
     ap.add_argument('--dtype', default='bfloat16', choices=['bfloat16', 'float32'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-kernel-timing', action='store_true')
+    ap.add_argument('--workload', default='iddpm', choices=['iddpm', 'mh'],
+                    help='iddpm: BASELINE configs[1] (the metric); mh: configs[2] MH/SRTM2 baseline')
+    ap.add_argument('--mh-chains', type=int, default=10000)
+    ap.add_argument('--mh-iters', type=int, default=20000, help='MH steps (draws) per chain')
+    ap.add_argument('--mh-tune', type=int, default=0)
     return ap.parse_args()
+
+
+def host_threads():
+    """CPU threads for the baseline leg: the job's CPU share (OMP_NUM_THREADS on the GPU
+    box, 16 per GPU), never the whole machine's core count."""
+    try:
+        n = int(os.environ.get('OMP_NUM_THREADS', '0'))
+    except ValueError:
+        n = 0
+    if n <= 0:
+        n = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else (os.cpu_count() or 1)
+    return max(1, min(n, 16))
 
 
 def cpu_baseline(weights, cond, budget_s=15.0):
     """Oracle (NumPy fp32 restatement) on a bounded sample: B=32 samples, as many reverse
-    steps as fit in ~budget_s, extrapolated to the 1000-step process."""
+    steps as fit in ~budget_s, extrapolated to the 1000-step process.  BLAS threads are
+    limited to the job's CPU share (host_threads)."""
     from oracle import iddpm_ref as R
+    cores = host_threads()
     try:
-        from threadpoolctl import threadpool_info
-        cores = max([p.get('num_threads', 1) for p in threadpool_info()] or [1])
+        from threadpoolctl import threadpool_limits
+        limiter = threadpool_limits(cores)
     except Exception:
-        cores = os.cpu_count() or 1
+        limiter = None
     S = R.schedule_tables(R.get_beta_schedule('cosine', 1000))
     rng = np.random.default_rng(0)
     B = 32
@@ -71,6 +90,8 @@ def cpu_baseline(weights, cond, budget_s=15.0):
         if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
+    if limiter is not None:
+        limiter.unregister()
     per_step = dt / n
     return {'value': B / (per_step * 1000.0), 'unit': 'samples/s', 'cores': int(cores), 'kind': 'port',
             'sample': f'oracle/iddpm_ref.py NumPy fp32, B=32 samples x {n} reverse steps ({dt:.1f} s), '
@@ -88,8 +109,95 @@ def load_traffic():
         return None
 
 
+# MH cost per element update (one ROI's SRTM2 + 54 truncated-normal terms), counted
+# from mh_kernels.hip: 54x54 operator FMAs + per-frame exp/sqrt/div/log/erfc/log.
+MH_FP64_FLOP_PER_UPDATE = 2 * 54 * 54 + 54 * 120
+
+
+def mh_cpu_baseline(P, budget_s=12.0):
+    """oracle/mh_ref.c (C restatement, OpenMP over chains) on a bounded sample."""
+    from oracle import mh_c
+    prob = mh_c.MHProblem(**P)
+    threads = host_threads()
+    chains, iters = threads * 2, 10
+    t0 = time.perf_counter()
+    prob.run(chains, iters, 0, seed=5, threads=threads)
+    dt = time.perf_counter() - t0
+    iters = max(10, int(iters * budget_s / max(dt, 1e-3)))
+    t0 = time.perf_counter()
+    prob.run(chains, iters, 0, seed=5, threads=threads)
+    dt = time.perf_counter() - t0
+    return {'value': chains * iters / dt, 'unit': 'chain-steps/s', 'cores': threads, 'kind': 'port',
+            'sample': f'oracle/mh_ref.c (gcc -O3, OpenMP), {chains} chains x {iters} steps ({dt:.1f} s)'}
+
+
+def main_mh(args):
+    """BASELINE configs[2]: MH/SRTM2, 48 ROI x 10k chains x 20k steps on one GPU
+    (weak scaling over ranks: every rank runs its own chains of its own TAC)."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    else:
+        torch.cuda.set_device(0)
+    from pet_posterior_distribution_amd.mcmc import MetropolisSRTM2
+    from pet_posterior_distribution_amd.sim_data import mh_problem
+    P = mh_problem(seed=rank)
+    mh = MetropolisSRTM2(**P)
+    n, iters, tune = args.mh_chains, args.mh_iters, args.mh_tune
+    mh.run(min(n, 2048), 2, 0, seed=1)                           # warm-up (module load)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    res = mh.run(n, iters, tune, seed=1 + rank)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], device='cuda', dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    # the reference's protocol per TAC (main_script.py:363-364; pymc default 4 chains):
+    # 4 chains x (20k draws + 40k tune), timed on a 1/50 slice and scaled
+    t1 = time.perf_counter()
+    mh.run(4, 400, 800, seed=3)
+    torch.cuda.synchronize()
+    ref_protocol_s = (time.perf_counter() - t1) * 50
+    if rank == 0:
+        steps = world * n * (iters + tune)
+        value = steps / elapsed
+        flops = steps * 96 * MH_FP64_FLOP_PER_UPDATE / elapsed / 1e12
+        line = {
+            'metric': 'MH chain-steps/sec (48-ROI SRTM2, element-wise Metropolis)', 'value': round(value, 1),
+            'unit': 'chain-steps/s', 'n_gpus': world, 'steps': 1, 'warmup': 1,
+            'ms_per_step': round(elapsed * 1e3, 3), 'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic (SRTM2 TAC + noise model, synthetic priors)',
+            'config': {'workload': 'mcmc.py Metropolis-Hastings, 48 ROI x 2 params, SRTM2', 'chains_per_gpu': n,
+                       'steps_per_chain': iters + tune, 'tune': tune},
+            'roofline': {'bound': 'valu-fp64', 'achieved': round(flops, 2), 'peak': 78.6, 'unit': 'TFLOP/s',
+                         'frac': round(flops / 78.6, 4), 'traffic': None,
+                         'flop_per_update': MH_FP64_FLOP_PER_UPDATE},
+            'mean_accept_rate': round(float(res['accept_rate'].mean()), 4),
+            'reference_protocol_per_tac_s': round(ref_protocol_s, 2),
+        }
+        line['cpu_baseline'] = None if (world > 1 or args.no_cpu_baseline) else mh_cpu_baseline(P)
+        print(json.dumps(line), flush=True)
+    mh.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.workload == 'mh':
+        return main_mh(args)
     import torch
     import torch.distributed as dist
     world = int(os.environ.get('WORLD_SIZE', '1'))

@@ -11,9 +11,14 @@
  * Model (mcmc.py:147-155): DVR ~ MvNormal(mu_DVR, Cov_DVR), R1 ~ MvNormal(mu_R1,
  * Cov_R1) (48-d each), k2' fixed, sn = SRTM2(DVR, R1, k2').T with sn < 0 -> 1e-6,
  * y_obs ~ TruncatedNormal(mu = sn, sigma = sqrt(sn) * sigma_noise, lower = 0).
- * Sampler: PyMC 5.12 Metropolis with NormalProposal, element-wise updates of the
- * 96 coordinates (DVR then R1), per-element scaling tuned every 100 tuning draws
- * with PyMC's tune table.  One 64-lane wavefront per chain (lane = frame /
+ * Sampler: PyMC 5.12 Metropolis with NormalProposal (Metropolis.astep with
+ * elemwise_update): per draw one proposal vector delta = N(0,1) * scaling over the
+ * 96 coordinates (DVR | R1), the coordinates visited in a freshly shuffled order,
+ * each coordinate's log ratio taken against the sweep-start point (pymc's
+ * delta_logp(q_temp, q0)) and accepted iff finite and log u < ratio
+ * (metrop_select); per-element scaling tuned every 100 tuning draws with PyMC's
+ * tune table.  PyMC is not vendored in the reference: this restates its
+ * published source (parity with PyMC itself unpinned).  One 64-lane wavefront per chain (lane = frame /
  * ROI), fp64 throughout (mcmc.py:22).  Draws are reduced on the GPU into
  * per-chain Welford accumulators instead of being stored.
  *
@@ -65,6 +70,11 @@ int petmh_destroy(petmh_handle h);
  * last_dev: [n_chains][2*n_roi] final state (may be NULL). */
 int petmh_run(petmh_handle h, const double* x0_dev, int n_chains, int n_draws, int n_tune, uint64_t seed,
               double* stats_dev, double* accept_dev, double* last_dev, void* stream);
+
+/* Sampler options (defaults = pymc Metropolis: tune_interval 100, scaling 1.0,
+ * vs_sweep_start 1).  vs_sweep_start 0 compares each element against the running
+ * state instead (textbook component-wise MH). */
+int petmh_set_sampler(petmh_handle h, int tune_interval, double scaling, int vs_sweep_start);
 
 /* Joint log density of mcmc.py:147-155 at n points x_dev [n][2*n_roi] -> out_dev [n]. */
 int petmh_logp(petmh_handle h, const double* x_dev, int n, double* out_dev, void* stream);

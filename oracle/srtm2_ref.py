@@ -9,8 +9,11 @@ Restates, in float64 NumPy:
 * kinetic_model.SRTM2.create_activity_curve  kinetic_model.py:142-158
 * the MH model of mcmc.py:147-155 (log posterior) and PyMC's element-wise
   Metropolis with NormalProposal and tune_interval=100 scaling (pymc 5.12,
-  requirements.txt:6; NOT vendored in the reference: restated from PyMC's
-  published algorithm, parity with PyMC itself is unpinned).
+  requirements.txt:6, ``Metropolis.astep`` with ``elemwise_update``: per draw one
+  proposal vector, shuffled element order, each element's ratio taken against
+  the sweep-start point).  PyMC is NOT vendored in the reference and is not
+  installed here: restated from PyMC's published source, parity with PyMC
+  itself is unpinned.
 
 Pinning: SRTM2 and the interpolation are checked bit-for-bit-close (1e-12)
 against the imported reference kinetic_model (tests/golden/g2_srtm2.npz,
@@ -121,66 +124,96 @@ def pymc_tune(scale, acc_rate):
                                         scale * 1.1], scale)
 
 
-def metropolis_elemwise(logp, x0, n_draws, n_tune, rng, tune_interval=100, scaling=1.0):
-    """PyMC 5.12 Metropolis(NormalProposal) with element-wise updates of a vector variable:
-    every draw proposes x_i + N(0,1) * s_i for each element in turn and accepts with
-    prob min(1, exp(logp' - logp)); during tuning s is rescaled every tune_interval
-    draws from the per-element acceptance rate (pymc_tune)."""
+def _pymc_sweep(logp, x, lp0, q, order, log_u, tune_acc, kept_acc, keep, vs_sweep_start=True):
+    """One Metropolis.astep with element-wise updates (pymc 5.12 metropolis.py):
+    q = x + delta was drawn for every element up front; elements are visited in the
+    shuffled `order`; element k's proposal is the running state with q[k] swapped in,
+    and -- as in pymc's ``delta_logp(q_temp, q0)`` -- it is compared against the
+    sweep-START state x (vs_sweep_start=False: against the running state).
+    metrop_select accepts iff the ratio is finite and log u < ratio."""
+    q_temp = x.copy()
+    lp_run = lp0
+    for k in order:
+        q_temp[k] = q[k]
+        lpp = logp(q_temp)
+        mr = lpp - (lp0 if vs_sweep_start else lp_run)
+        if np.isfinite(mr) and log_u[k] < mr:
+            lp_run = lpp
+            tune_acc[k] += 1
+            if keep:
+                kept_acc[k] += 1
+        else:
+            q_temp[k] = x[k]
+    return q_temp, lp_run
+
+
+def metropolis_elemwise(logp, x0, n_draws, n_tune, rng, tune_interval=100, scaling=1.0, vs_sweep_start=True):
+    """PyMC 5.12 Metropolis(NormalProposal) on a vector variable (elemwise_update):
+    per draw: tune (every tune_interval tuning draws, per-element pymc_tune on the
+    acceptance rate), delta = N(0,1) * scaling for all elements, shuffle the element
+    order, then the element-wise accept/reject sweep of _pymc_sweep."""
     x = np.array(x0, dtype=np.float64)
-    lp = logp(x)
-    s = np.full(x.shape, float(scaling))
-    acc = np.zeros(x.shape)
+    n = x.size
+    s = np.full(n, float(scaling))
+    acc = np.zeros(n)
+    kept = np.zeros(n)
     out = np.empty((n_draws,) + x.shape)
     for it in range(n_tune + n_draws):
         if it < n_tune and it > 0 and it % tune_interval == 0:
             s = pymc_tune(s, acc / tune_interval)
             acc[:] = 0
-        for i in range(x.size):
-            prop = x.copy()
-            prop[i] += rng.standard_normal() * s[i]
-            lpp = logp(prop)
-            if np.log(rng.uniform()) < lpp - lp:
-                x, lp = prop, lpp
-                acc[i] += 1
+        q = x + rng.standard_normal(n) * s
+        order = rng.permutation(n)
+        log_u = np.log(rng.uniform(size=n))
+        x, _ = _pymc_sweep(logp, x, logp(x), q, order, log_u, acc, kept, it >= n_tune, vs_sweep_start)
         if it >= n_tune:
             out[it - n_tune] = x
     return out
 
 
-def philox_mh_noise(seed, chain, it, k):
-    """The GPU sampler's counter-based draws for element k of iteration `it` of `chain`:
-    Philox4x32-10(counter = (k, it, chain_lo, chain_hi), key = seed) -> N(0,1) proposal
-    (Box-Muller of words 0, 1) and the accept uniform (word 2)."""
+def philox_mh_block(seed, chain, it, k):
+    """The GPU sampler's counter-based draws for element k of sweep `it` of `chain`:
+    Philox4x32-10(counter = (k, it, chain_lo, chain_hi), key = seed) -> N(0,1)
+    proposal (Box-Muller cos of words 0, 1), accept uniform (word 2) and the
+    element's sort key for the sweep's shuffled order (word 3)."""
     from oracle.iddpm_ref import philox4x32_10
     q = philox4x32_10(k, it, chain & 0xffffffff, chain >> 32, seed & 0xffffffff, (seed >> 32) & 0xffffffff)
     u1 = (float(q[0]) + 1.0) * 2.0 ** -32
     u2 = (float(q[1]) + 0.5) * 2.0 ** -32
     ua = (float(q[2]) + 0.5) * 2.0 ** -32
-    return np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * u2), ua
+    return np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * u2), ua, int(q[3])
 
 
-def metropolis_elemwise_philox(logp, x0, n_draws, n_tune, seed, chain, tune_interval=100, scaling=1.0):
+def philox_mh_noise(seed, chain, it, k):
+    z, ua, _ = philox_mh_block(seed, chain, it, k)
+    return z, ua
+
+
+def philox_sweep(seed, chain, it, n=96):
+    """(z[n], ua[n], order): order = elements by ascending (word-3 key, index)."""
+    blk = [philox_mh_block(seed, chain, it, k) for k in range(n)]
+    z = np.array([b[0] for b in blk])
+    ua = np.array([b[1] for b in blk])
+    keys = np.array([b[2] for b in blk], dtype=np.uint64)
+    return z, ua, np.argsort(keys, kind='stable')
+
+
+def metropolis_elemwise_philox(logp, x0, n_draws, n_tune, seed, chain, tune_interval=100, scaling=1.0,
+                               vs_sweep_start=True):
     """metropolis_elemwise with the GPU sampler's noise stream (identical chain path)."""
     x = np.array(x0, dtype=np.float64)
-    lp = logp(x)
-    s = np.full(x.shape, float(scaling))
-    acc = np.zeros(x.shape)
-    kept_acc = np.zeros(x.shape)
+    n = x.size
+    s = np.full(n, float(scaling))
+    acc = np.zeros(n)
+    kept = np.zeros(n)
     out = np.empty((n_draws,) + x.shape)
     for it in range(n_tune + n_draws):
         if it < n_tune and it > 0 and it % tune_interval == 0:
             s = pymc_tune(s, acc / tune_interval)
             acc[:] = 0
-        for k in range(x.size):
-            z, ua = philox_mh_noise(seed, chain, it, k)
-            prop = x.copy()
-            prop[k] += z * s[k]
-            lpp = logp(prop)
-            if np.log(ua) < lpp - lp:
-                x, lp = prop, lpp
-                acc[k] += 1
-                if it >= n_tune:
-                    kept_acc[k] += 1
+        z, ua, order = philox_sweep(seed, chain, it, n)
+        x, _ = _pymc_sweep(logp, x, logp(x), x + z * s, order, np.log(ua), acc, kept, it >= n_tune,
+                           vs_sweep_start)
         if it >= n_tune:
             out[it - n_tune] = x
-    return out, kept_acc
+    return out, kept

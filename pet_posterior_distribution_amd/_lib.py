@@ -62,6 +62,7 @@ SYMBOLS = [
     ('petmh_destroy', C.c_int, [C.c_void_p]),
     ('petmh_run', C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_p, C.c_void_p,
                             C.c_void_p, C.c_void_p]),
+    ('petmh_set_sampler', C.c_int, [C.c_void_p, C.c_int, C.c_double, C.c_int]),
     ('petmh_logp', C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
     ('petmh_last_error', C.c_char_p, []),
 ]

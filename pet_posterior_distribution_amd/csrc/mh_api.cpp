@@ -144,6 +144,9 @@ struct petmh_ctx {
   int device = 0;
   Buf M, PD, PR, Y, SIG, CR, TV, MUD, MUR;
   MHConst c{};
+  int tune_interval = 100;   // pymc Metropolis defaults
+  double scaling = 1.0;
+  int vs_sweep_start = 1;    // pymc 5.12 elemwise_update compares against the sweep-start point
 };
 
 extern "C" {
@@ -218,13 +221,22 @@ int petmh_run(petmh_handle h, const double* x0, int n_chains, int n_draws, int n
   r.n_chains = n_chains;
   r.n_draws = n_draws;
   r.n_tune = n_tune;
-  r.tune_interval = 100;   // pymc Metropolis default
-  r.scaling = 1.0;         // pymc Metropolis default
+  r.tune_interval = h->tune_interval;
+  r.scaling = h->scaling;
+  r.vs_sweep_start = h->vs_sweep_start;
   r.seed = seed;
   r.stats = stats;
   r.accept = accept;
   r.last = last;
   HIPC(launch_mh_chains(h->c, r, (hipStream_t)stream));
+  return 0;
+}
+
+int petmh_set_sampler(petmh_handle h, int tune_interval, double scaling, int vs_sweep_start) {
+  if (!h || tune_interval <= 0 || !(scaling > 0.0)) return fail("bad sampler options");
+  h->tune_interval = tune_interval;
+  h->scaling = scaling;
+  h->vs_sweep_start = vs_sweep_start != 0;
   return 0;
 }
 

@@ -26,6 +26,7 @@ struct MHConst {               // device pointers, fp64
 struct MHRun {
   const double* x0;            // [n_chains][96] or null
   int n_chains, n_draws, n_tune, tune_interval;
+  int vs_sweep_start;          // pymc 5.12: ratios against the sweep-start point
   double scaling;
   unsigned long long seed;
   double* stats;               // [n_chains][96][3]

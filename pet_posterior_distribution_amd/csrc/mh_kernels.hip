@@ -21,6 +21,10 @@ struct Lds {
   double CR[NF], TV[NF];
   double MUD[NR], MUR[NR];
   double E[kWaves][64];               // per-wave exponential scratch
+  double Z[kWaves][2 * NR];           // per-wave sweep draws: N(0,1) proposal per element
+  double LU[kWaves][2 * NR];          //   log accept-uniform per element
+  uint32_t KEY[kWaves][2 * NR];       //   sort key of the shuffled order
+  int ORD[kWaves][2 * NR];            //   the sweep's element order
 };
 
 // Butterfly sum; lanes may differ in the last bit (different pairing order), so the
@@ -90,13 +94,25 @@ __device__ __forceinline__ double tune_scale(double s, double rate) {   // pymc 
   return s;
 }
 
+// One chain per wavefront.  Per draw (pymc 5.12 Metropolis.astep, elemwise_update):
+// tune, draw the proposal vector + accept uniforms + the shuffled element order for
+// all 96 elements in parallel (lane k: Philox block of element k), then the sequential
+// element-wise sweep.  Element k = (v, i): v = 0 DVR / 1 R1, ROI i.  A proposal for
+// ROI i changes only ROI i's TAC, so its log ratio vs the running state is
+// d_prior + ll_i(new) - ll_i; pymc compares against the sweep-START point, i.e. adds
+// the running sum `run` of the sweep's accepted ratios (vs_sweep_start).
 __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun r) {
   __shared__ Lds s;
   load_lds(s, c);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   double* e = s.E[w];
+  double* Zw = s.Z[w];
+  double* LUw = s.LU[w];
+  uint32_t* KEYw = s.KEY[w];
+  int* ORDw = s.ORD[w];
   const bool own = lane < NR;
   const int li = own ? lane : 0;
+  const uint32_t sk0 = (uint32_t)(r.seed & 0xffffffffull), sk1 = (uint32_t)(r.seed >> 32);
   for (int chain = blockIdx.x * kWaves + w; chain < r.n_chains; chain += gridDim.x * kWaves) {
     // ---- state: lane l < 48 holds ROI l
     double D = r.x0 ? r.x0[(size_t)chain * 2 * NR + li] : s.MUD[li];
@@ -126,6 +142,8 @@ __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun 
     double accD = 0.0, accR = 0.0;       // accepts over kept draws
     double mD = 0.0, m2D = 0.0, mR = 0.0, m2R = 0.0;
     long long nk = 0;
+    const uint32_t ch_lo = (uint32_t)((unsigned long long)chain & 0xffffffffull);
+    const uint32_t ch_hi = (uint32_t)((unsigned long long)chain >> 32);
     const int total = r.n_tune + r.n_draws;
     for (int it = 0; it < total; ++it) {
       if (it < r.n_tune && it > 0 && it % r.tune_interval == 0) {
@@ -133,42 +151,70 @@ __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun 
         sR = tune_scale(sR, (double)aR / r.tune_interval);
         aD = aR = 0;
       }
-#pragma unroll 1
-      for (int v = 0; v < 2; ++v) {
-        const double* P = v == 0 ? s.PD : s.PR;
-#pragma unroll 1
-        for (int i = 0; i < NR; ++i) {
-          uint32_t q[4] = {(uint32_t)(v * NR + i), (uint32_t)it, (uint32_t)((unsigned long long)chain & 0xffffffffull),
-                           (uint32_t)((unsigned long long)chain >> 32)};
-          philox(q, (uint32_t)(r.seed & 0xffffffffull), (uint32_t)(r.seed >> 32));
+      // ---- the draw's random numbers, element k on lane k (and k - 64 for k >= 64)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = lane + 64 * h;
+        if (k < 2 * NR) {
+          uint32_t q[4] = {(uint32_t)k, (uint32_t)it, ch_lo, ch_hi};
+          philox(q, sk0, sk1);
           const double u1 = ((double)q[0] + 1.0) * 2.3283064365386963e-10;
           const double u2 = ((double)q[1] + 0.5) * 2.3283064365386963e-10;
-          const double ua = ((double)q[2] + 0.5) * 2.3283064365386963e-10;
-          const double zz = sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
-          const double xi = __shfl(v == 0 ? D : R, i, 64);
-          const double si = __shfl(v == 0 ? sD : sR, i, 64);
-          const double gi = __shfl(v == 0 ? gD : gR, i, 64);
-          const double lli = __shfl(ll, i, 64);
-          const double delta = zz * si;
-          const double xp = xi + delta;
-          const double dprior = -0.5 * (2.0 * delta * gi + delta * delta * P[i * NR + i]);
-          const double dn = v == 0 ? xp : __shfl(D, i, 64);
-          const double rn = v == 0 ? __shfl(R, i, 64) : xp;
-          const double lln = roi_loglik(s, e, lane, i, dn, rn, c.k2p);
-          const double logacc = dprior + lln - lli;
-          if (log(ua) < logacc) {          // wave-uniform decision
-            if (lane == i) {
-              if (v == 0) { D = xp; aD += 1; if (it >= r.n_tune) accD += 1.0; }
-              else { R = xp; aR += 1; if (it >= r.n_tune) accR += 1.0; }
-              ll = lln;
-            }
-            if (own) {
-              if (v == 0) gD = fma(delta, P[lane * NR + i], gD);
-              else gR = fma(delta, P[lane * NR + i], gR);
-            }
+          Zw[k] = sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
+          LUw[k] = log(((double)q[2] + 0.5) * 2.3283064365386963e-10);
+          KEYw[k] = q[3];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      // ---- shuffled order: rank of (key, k) among the 96 elements
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = lane + 64 * h;
+        if (k < 2 * NR) {
+          const uint32_t kk = KEYw[k];
+          int rank = 0;
+#pragma unroll 8
+          for (int j = 0; j < 2 * NR; ++j) {
+            const uint32_t kj = KEYw[j];
+            rank += (kj < kk) | ((kj == kk) & (j < k));
+          }
+          ORDw[rank] = k;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      double run = 0.0;                  // log p(running) - log p(sweep start)
+#pragma unroll 1
+      for (int j = 0; j < 2 * NR; ++j) {
+        const int k = ORDw[j];
+        const int v = k >= NR, i = v ? k - NR : k;
+        const double* P = v ? s.PR : s.PD;
+        const double Di = __shfl(D, i, 64), Ri = __shfl(R, i, 64);
+        const double xi = v ? Ri : Di;
+        const double si = __shfl(v ? sR : sD, i, 64);
+        const double gi = __shfl(v ? gR : gD, i, 64);
+        const double lli = __shfl(ll, i, 64);
+        const double delta = Zw[k] * si;
+        const double xp = xi + delta;
+        const double dprior = -0.5 * (2.0 * delta * gi + delta * delta * P[i * NR + i]);
+        const double lln = roi_loglik(s, e, lane, i, v ? Di : xp, v ? xp : Ri, c.k2p);
+        const double step = dprior + lln - lli;
+        const double mr = r.vs_sweep_start ? run + step : step;
+        if (isfinite(mr) && LUw[k] < mr) {   // wave-uniform decision (metrop_select)
+          run += step;
+          if (lane == i) {
+            if (v == 0) { D = xp; aD += 1; if (it >= r.n_tune) accD += 1.0; }
+            else { R = xp; aR += 1; if (it >= r.n_tune) accR += 1.0; }
+            ll = lln;
+          }
+          if (own) {
+            if (v == 0) gD = fma(delta, P[lane * NR + i], gD);
+            else gR = fma(delta, P[lane * NR + i], gR);
           }
         }
       }
+      __builtin_amdgcn_wave_barrier();
       if (it >= r.n_tune) {              // Welford over kept draws
         ++nk;
         const double dd = D - mD;

@@ -3,7 +3,9 @@
 ``MetropolisSRTM2`` holds one test TAC's problem (mcmc.py:73-137: frame times,
 reference TAC, fixed k2', observed y = tac_noisy / dt, noise sigmas, MvNormal
 priors) and runs many independent chains of PyMC 5.12's element-wise
-Metropolis(NormalProposal) with tune_interval = 100 on the GPU (one wavefront per
+Metropolis(NormalProposal) with tune_interval = 100 on the GPU (shuffled
+element order per draw, ratios against the sweep-start point as in pymc's
+``Metropolis.astep``) (one wavefront per
 chain, include/petmh.h).  Draws are reduced on the device to Welford partials;
 ``run`` returns the pooled posterior mean / population std per ROI (the
 quantities the reference compares against iDDPM, main_script.py:719-805).
@@ -21,7 +23,8 @@ from .distributed import merge_stats
 
 
 class MetropolisSRTM2:
-    def __init__(self, time_vector, tac_ref, k2p, y_obs, sigma_noise, mu_DVR, Cov_DVR, mu_R1, Cov_R1, device=None):
+    def __init__(self, time_vector, tac_ref, k2p, y_obs, sigma_noise, mu_DVR, Cov_DVR, mu_R1, Cov_R1, device=None,
+                 tune_interval=100, scaling=1.0, vs_sweep_start=True):
         self.device = torch.device('cuda', device if device is not None else torch.cuda.current_device())
         arr = lambda a: np.ascontiguousarray(a, dtype=np.float64)   # noqa: E731
         self._keep = [arr(time_vector), arr(tac_ref), arr(y_obs), arr(sigma_noise), arr(mu_DVR), arr(Cov_DVR),
@@ -35,6 +38,8 @@ class MetropolisSRTM2:
         torch.cuda.set_device(self.device)
         _lib.check_mh(_lib.lib().petmh_create(C.byref(p), self.device.index, C.byref(h)), 'petmh_create')
         self._h = h
+        _lib.check_mh(_lib.lib().petmh_set_sampler(h, int(tune_interval), float(scaling), int(bool(vs_sweep_start))),
+                      'petmh_set_sampler')
 
     def close(self):
         if getattr(self, '_h', None) is not None:

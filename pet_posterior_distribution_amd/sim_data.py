@@ -134,3 +134,13 @@ def make_condition(seed=0, prior=None, mean_sigma_noise=0.1, return_truth=False)
         return cond, dict(DVR=DVR, R1=R1, k2p=prior['mu_k2p'], tac_ref=ref, tac=tac,
                           sigma_noise=sigma_noise, time_vector=tv, dt=dt)
     return cond
+
+
+def mh_problem(seed=0, prior=None, mean_sigma_noise=0.1):
+    """The MH inputs of one synthetic test TAC (mcmc.py:73-137): frame times, reference
+    TAC, fixed k2', y_obs, per-frame noise sigmas and the MvNormal priors."""
+    prior = prior or synthetic_prior()
+    cond, truth = make_condition(seed, prior, mean_sigma_noise, return_truth=True)
+    return dict(time_vector=truth['time_vector'], tac_ref=truth['tac_ref'], k2p=float(truth['k2p']),
+                y_obs=cond[:N_ROI].astype(np.float64), sigma_noise=truth['sigma_noise'],
+                mu_DVR=prior['mu_DVR'], Cov_DVR=prior['Cov_DVR'], mu_R1=prior['mu_R1'], Cov_R1=prior['Cov_R1'])

@@ -43,6 +43,14 @@ def main(d, out=None):
         print(k, {c: round(v, 1) for c, v in res[k].items()})
     if out:
         json.dump(res, open(out, 'w'), indent=1)
+        ub = res.get('up0.block', {})
+        if 'hbm_read_bytes_corrected' in ub and 'hbm_write_bytes' in ub:
+            tr = {'up0_block_bytes_per_launch': ub['hbm_read_bytes_corrected'] + ub['hbm_write_bytes'],
+                  'read_bytes': ub['hbm_read_bytes_corrected'], 'write_bytes': ub['hbm_write_bytes'],
+                  'source': os.path.relpath(out, os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                  'method': 'rocprofv3 --pmc FETCH_SIZE (x2, gfx950 64-B tally) + WRITE_SIZE, KB->B, mean per dispatch'}
+            json.dump(tr, open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                            'profiles', 'pmc_traffic.json'), 'w'), indent=1)
     return res
 
 
