@@ -47,8 +47,8 @@ def parse():
     ap.add_argument('--workload', default='iddpm', choices=['iddpm', 'mh'],
                     help='iddpm: BASELINE configs[1] (the metric); mh: configs[2] MH/SRTM2 baseline')
     ap.add_argument('--mh-chains', type=int, default=10000)
-    ap.add_argument('--mh-iters', type=int, default=20000, help='MH steps (draws) per chain')
-    ap.add_argument('--mh-tune', type=int, default=0)
+    ap.add_argument('--mh-iters', type=int, default=10000, help='MH draws per chain (kept)')
+    ap.add_argument('--mh-tune', type=int, default=10000, help='MH tuning steps per chain (config 3: 20k steps in total)')
     return ap.parse_args()
 
 

@@ -370,6 +370,8 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
     a.tac = io.tac;
     a.tvec = io.tvec;
     a.t_uniform = io.t_uniform;
+    a.n_t = h->T;
+    a.n_tac = h->n_tac;
     a.B = B;
     a.cout = cl.cout;
     if (li == kNumConvLayers - 1) a.fin = io.fin;

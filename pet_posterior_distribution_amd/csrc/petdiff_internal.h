@@ -63,6 +63,7 @@ struct ConvArgs {
   const int* tvec;           // [B] timestep per sample (used when t_uniform < 0)
   int t_uniform;
   int B, cout;
+  int n_t, n_tac;            // rows of tmap / cmap (buffer bounds of the epilogue map prefetch)
   FinalArgs fin;
 };
 

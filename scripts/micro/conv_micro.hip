@@ -1,0 +1,150 @@
+// Micro-benchmark of the conv layers in isolation (diagnostic, not the product).
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -DCONV_EXP_MODE=<m> conv_micro.hip
+// Prints avg us per launch for each layer over random bf16 data.
+#include "../../pet_posterior_distribution_amd/csrc/unet_kernels.hip"
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <algorithm>
+
+using namespace petdiff;
+
+__global__ void fill_bf16(bf16* p, size_t n, unsigned seed) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    unsigned h = (unsigned)i * 2654435761u ^ seed;
+    h ^= h >> 13; h *= 0x5bd1e995u; h ^= h >> 15;
+    p[i] = (bf16)(((int)(h & 0xffff) - 32768) * (1.0f / 65536.f));
+  }
+}
+__global__ void fill_f32(float* p, size_t n, unsigned seed) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    unsigned h = (unsigned)i * 2654435761u ^ seed;
+    h ^= h >> 13; h *= 0x5bd1e995u; h ^= h >> 15;
+    p[i] = ((int)(h & 0xffff) - 32768) * (1.0f / 65536.f);
+  }
+}
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+template <int KIND>
+void run(const char* name, int B, int c1, int c2, int cout, int iters) {
+  using G = ConvGeom<bf16, KIND>;
+  const size_t rows_in = (size_t)B * G::LIN, rows_out = (size_t)B * G::L;
+  const int NC = c1 / G::KC + c2 / G::KC;
+  bf16 *s1, *s2 = nullptr, *w, *out, *pool;
+  float *cmap, *tmap, *bias;
+  CK(hipMalloc(&s1, rows_in * c1 * 2));
+  if (c2) CK(hipMalloc(&s2, rows_in * c2 * 2));
+  const size_t wbytes = (size_t)(cout / G::NT) * NC * G::B_BYTES;
+  CK(hipMalloc(&w, wbytes));
+  CK(hipMalloc(&out, rows_out * cout * 2));
+  CK(hipMalloc(&pool, rows_out * cout));
+  CK(hipMalloc(&cmap, (size_t)G::L * cout * 4));
+  CK(hipMalloc(&tmap, (size_t)1000 * G::L * cout * 4));
+  CK(hipMalloc(&bias, cout * 4));
+  fill_bf16<<<1024, 256>>>(s1, rows_in * c1, 1);
+  if (c2) fill_bf16<<<1024, 256>>>(s2, rows_in * c2, 2);
+  fill_bf16<<<1024, 256>>>(w, wbytes / 2, 3);
+  fill_f32<<<1024, 256>>>(cmap, (size_t)G::L * cout, 4);
+  fill_f32<<<1024, 256>>>(tmap, (size_t)1000 * G::L * cout, 5);
+  fill_f32<<<64, 256>>>(bias, cout, 6);
+  // final-epilogue buffers
+  float *wf, *bfv, *xt, *xn, *tab;
+  unsigned long long* rng;
+  CK(hipMalloc(&wf, 128 * 4 * 4));
+  CK(hipMalloc(&bfv, 16));
+  CK(hipMalloc(&xt, (size_t)B * 96 * 4));
+  CK(hipMalloc(&xn, (size_t)B * 96 * 4));
+  CK(hipMalloc(&tab, (size_t)kNTab * 1000 * 4));
+  CK(hipMalloc(&rng, 16));
+  fill_f32<<<64, 256>>>(wf, 512, 7);
+  fill_f32<<<64, 256>>>(bfv, 4, 8);
+  fill_f32<<<256, 256>>>(xt, (size_t)B * 96, 9);
+  fill_f32<<<256, 256>>>(tab, (size_t)kNTab * 1000, 10);
+  CK(hipMemset(rng, 0, 16));
+  ConvArgs<bf16> a{};
+  a.src1 = s1; a.c1 = c1; a.src2 = s2; a.c2 = c2; a.wpack = w; a.out = out; a.out_pool = pool;
+  a.cmap = cmap; a.tmap = tmap; a.bias = bias; a.tac = nullptr; a.tvec = nullptr; a.t_uniform = 500;
+  a.B = B; a.cout = cout; a.n_t = 1000; a.n_tac = 1;
+  a.fin.wf = wf; a.fin.bf = bfv; a.fin.n_out = 4; a.fin.x_t = xt; a.fin.z = nullptr; a.fin.rng = rng;
+  a.fin.rng_step = 3; a.fin.tab = tab; a.fin.T = 1000; a.fin.learn_mode = 2; a.fin.param_mode = 0;
+  a.fin.flag_var_tilde = 1; a.fin.x_next = xn;
+  unsigned long long* dbg;
+  CK(hipMalloc(&dbg, 6 * 4096 * 8));
+  CK(hipMemset(dbg, 0, 6 * 4096 * 8));
+#if CONV_EXP_MODE & 128
+  a.fin.x_all = reinterpret_cast<float*>(dbg);
+#endif
+  CK(hipDeviceSynchronize());
+  for (int i = 0; i < 20; ++i) CK(launch_conv<bf16>(KIND, a, 0));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0, 0));
+  for (int i = 0; i < iters; ++i) CK(launch_conv<bf16>(KIND, a, 0));
+  CK(hipEventRecord(e1, 0));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  const double us = ms * 1e3 / iters;
+#if CONV_EXP_MODE & 128
+  {
+    const int nb = ((B + G::S - 1) / G::S) * (cout / G::NT);
+    std::vector<unsigned long long> h(2 * nb);
+    CK(hipMemcpy(h.data(), dbg, 2 * nb * 8, hipMemcpyDeviceToHost));
+    std::vector<double> cyc, clk;
+    for (int b = 0; b < nb; ++b) { cyc.push_back((double)h[2 * b]); clk.push_back(h[2 * b] / (h[2 * b + 1] * 1e-8) * 1e-9); }
+    std::sort(cyc.begin(), cyc.end());
+    std::sort(clk.begin(), clk.end());
+    const double nmfma = (double)(c1 + c2) / G::KC * G::TAPS * (G::ROWB / 32) * 6;
+    std::vector<unsigned long long> t4(4 * nb);
+    CK(hipMemcpy(t4.data(), dbg + 8192, 4 * nb * 8, hipMemcpyDeviceToHost));
+    unsigned long long tmin = ~0ull, tmax = 0;
+    std::vector<double> pro, lp, epi, st;
+    for (int b = 0; b < nb; ++b) tmin = std::min(tmin, t4[4 * b]);
+    for (int b = 0; b < nb; ++b) {
+      tmax = std::max(tmax, t4[4 * b + 3]);
+      st.push_back((t4[4 * b] - tmin) * 0.01);
+      pro.push_back((t4[4 * b + 1] - t4[4 * b]) * 0.01);
+      lp.push_back((t4[4 * b + 2] - t4[4 * b + 1]) * 0.01);
+      epi.push_back((t4[4 * b + 3] - t4[4 * b + 2]) * 0.01);
+    }
+    std::vector<unsigned long long> e2(2 * nb);
+    CK(hipMemcpy(e2.data(), dbg + 4096, 2 * nb * 8, hipMemcpyDeviceToHost));
+    std::vector<double> ea, eb, ec;
+    for (int b = 0; b < nb; ++b) {
+      ea.push_back((e2[2 * b] - t4[4 * b + 2]) * 0.01);
+      eb.push_back((e2[2 * b + 1] - e2[2 * b]) * 0.01);
+      ec.push_back((t4[4 * b + 3] - e2[2 * b + 1]) * 0.01);
+    }
+    auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
+    auto mx = [](std::vector<double> v) { return *std::max_element(v.begin(), v.end()); };
+    printf("   us: start skew max %.2f | prologue med %.2f max %.2f | loop med %.2f max %.2f | epilogue med %.2f max %.2f | span %.2f\n",
+           mx(st), med(pro), mx(pro), med(lp), mx(lp), med(epi), mx(epi), (tmax - tmin) * 0.01);
+    printf("   epilogue us: acc->LDS+barrier %.2f | read/add/store issue %.2f | store drain %.2f\n", med(ea), med(eb),
+           med(ec));
+    printf("   loop cycles median %.0f (%.1f per MFMA), clock median %.3f GHz [%.3f..%.3f]\n", cyc[nb / 2],
+           cyc[nb / 2] / nmfma, clk[nb / 2], clk[0], clk[nb - 1]);
+  }
+#endif
+  const double flop = 2.0 * rows_out * cout * (double)(c1 + c2) * G::TAPS;
+  printf("%-12s mode %d  %8.2f us  %7.1f TF/s (executed)  grid %d\n", name, CONV_EXP_MODE, us, flop / us * 1e-6,
+         ((B + G::S - 1) / G::S) * (cout / G::NT));
+  hipFree(s1); if (s2) hipFree(s2); hipFree(w); hipFree(out); hipFree(pool); hipFree(cmap); hipFree(tmap);
+  hipFree(bias); hipFree(wf); hipFree(bfv); hipFree(xt); hipFree(xn); hipFree(tab); hipFree(rng); hipFree(dbg);
+}
+
+int main(int argc, char** argv) {
+  const int B = argc > 1 ? atoi(argv[1]) : 1024;
+  const int it = 200;
+  run<LK_DOWN1>("down1", B, 128, 0, 256, it);
+  run<LK_DOWN2>("down2", B, 256, 0, 512, it);
+  run<LK_DOWN3>("down3", B, 512, 0, 1024, it);
+  run<LK_UP0_CONV2>("up0.conv2", B, 1024, 0, 512, it);
+  run<LK_UP0_BLOCK>("up0.block", B, 512, 512, 512, it);
+  run<LK_UP1_CONV2>("up1.conv2", B, 512, 0, 256, it);
+  run<LK_UP1_BLOCK>("up1.block", B, 256, 256, 256, it);
+  run<LK_UP2_CONV2>("up2.conv2", B, 256, 0, 128, it);
+  run<LK_UP2_BLOCK>("up2.block", B, 128, 128, 128, it);
+  return 0;
+}
