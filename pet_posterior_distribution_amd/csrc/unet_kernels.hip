@@ -20,6 +20,7 @@
 #include "petdiff_internal.h"
 
 #include <type_traits>
+#include <algorithm>
 
 // Diagnostic builds only (scripts/micro/conv_micro.hip): bit 1 drops the K-loop DMA,
 // bit 2 the MFMAs, bit 4 the epilogue, bit 8 returns at entry, bit 16 returns after
@@ -422,13 +423,15 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
         if constexpr (sizeof(T) == 2 && !(CONV_EXP_MODE & 2))
           acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[pb][i], bv[pb][jn], acc[i][jn], 0, 0, 0);
   };
+  // NEXT = 2 (first chunk only): the pieces of chunks nkc and nkc + 1 (stages nbuf, nbuf + 1).
   auto compute = [&](const char* base, auto next_tag, int nkc, int nbuf) {
-    constexpr bool NEXT = decltype(next_tag)::value;
+    constexpr int NEXT = (int)decltype(next_tag)::value;
     char* nbase = smem + nbuf * G::STAGE;
     if constexpr (sizeof(T) == 2) {
       constexpr int NG = ROWB / 32;
       constexpr int NS = TAPS * NG;
-      constexpr int PPS = (G::PER + NS - 1) / NS;   // DMA pieces per step
+      constexpr int NPC = (NEXT == 2 ? 2 : 1) * G::PER;   // pieces to issue over this chunk
+      constexpr int PPS = (NPC + NS - 1) / NS;            // DMA pieces per step
       static_assert(NS % 2 == 0, "fragment double buffer alternates per step");
 #pragma unroll
       for (int st = 0; st < NS; ++st) {
@@ -464,10 +467,13 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
         PETDIFF_MF(2, 1)
 #undef PETDIFF_RD
 #undef PETDIFF_MF
-        if constexpr (NEXT && !(CONV_EXP_MODE & 1)) {
+        if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
 #pragma unroll
-          for (int u = 0; u < PPS; ++u)
-            if (st * PPS + u < G::PER) dma.piece(nbase, st * PPS + u, nkc, lane);
+          for (int u = 0; u < PPS; ++u) {
+            const int k = st * PPS + u;
+            if (k < G::PER) dma.piece(nbase, k, nkc, lane);
+            else if (k < NPC) dma.piece(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
+          }
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -490,7 +496,8 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
             bv0[jn] = *reinterpret_cast<const f32x4*>(base + ((boff[jn] + j * NT * ROWB) ^ (g << 6)));
             bv1[jn] = *reinterpret_cast<const f32x4*>(base + ((boff[jn] + j * NT * ROWB) ^ (g << 6) ^ 16));
           }
-          if constexpr (NEXT) {
+          static_assert(NEXT != 2, "f32 path: one chunk in flight per compute");
+          if constexpr (NEXT != 0) {
             const int st = j * NG + g;
 #pragma unroll
             for (int u = 0; u < PPS; ++u)
@@ -514,8 +521,9 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
       }
     }
   };
-  using Yes = std::integral_constant<bool, true>;
-  using No = std::integral_constant<bool, false>;
+  using Yes = std::integral_constant<int, 1>;
+  using No = std::integral_constant<int, 0>;
+  using Two = std::integral_constant<int, 2>;
 
   // epilogue operands fetched before the K loop (latency hidden behind it)
   const int ep_cg = tid % (NT / 8), ep_nloc = ep_cg * 8;
@@ -576,10 +584,12 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
   } else {
     // 3-deep ring: chunk kc+2 is in flight while chunk kc is computed; the wait
     // before each barrier retires chunk kc+1 only (counted vmcnt, never 0 mid-loop).
+    // bf16: the prologue lands chunk 0 only; chunk 0's compute issues chunks 1 and 2.
+    constexpr bool EARLY = sizeof(T) == 2;
     dma.all(smem, 0, 0, lane);
-    if (NC > 1) dma.all(smem, 1, 1, lane);
+    if (!EARLY && NC > 1) dma.all(smem, 1, 1, lane);
     prefetch_maps();
-    if (NC > 1) {
+    if (!EARLY && NC > 1) {
       ring_barrier<G::PER>();
     } else {
       ring_barrier<0>();
@@ -593,23 +603,37 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
     st_c0 = __builtin_amdgcn_s_memtime();
     st_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    int buf = 0;
-    for (int kc = 0; kc + 2 < NC; ++kc) {
+    int buf = 0, kc = 0;
+    if constexpr (EARLY) {
+      if (NC >= 3) {
+        compute(smem, Two{}, 1, 1);                    // chunks 1, 2 -> stages 1, 2
+        ring_barrier<G::PER>();
+      } else if (NC == 2) {
+        compute(smem, Yes{}, 1, 1);
+        ring_barrier<0>();
+      }
+      if (NC >= 2) {
+        buf = 1;
+        kc = 1;
+      }
+    }
+    for (; kc + 2 < NC; ++kc) {
       const int nb = buf == 0 ? 2 : buf - 1;          // (kc + 2) % 3
       compute(smem + buf * G::STAGE, Yes{}, kc + 2, nb);
       ring_barrier<G::PER>();
       buf = buf == 2 ? 0 : buf + 1;
     }
     // tail: the last (up to) two chunks, nothing left to prefetch
-    if (NC >= 2) {
+    if (kc + 1 < NC) {
       compute(smem + buf * G::STAGE, No{}, 0, 0);
       ring_barrier<0>();
       buf = buf == 2 ? 0 : buf + 1;
     }
-    compute(smem + buf * G::STAGE, No{}, 0, 0);
-    ring_barrier<0>();
-  }
-  mfma_bf16(1);   // the last chunk's last step (NS even)
+    if (kc < NC) {
+      compute(smem + buf * G::STAGE, No{}, 0, 0);
+      ring_barrier<0>();
+    }
+  }  mfma_bf16(1);   // the last chunk's last step (NS even)
 #if CONV_EXP_MODE & 128
   if constexpr (G::STAGES == 3) {   // diagnostic: main-loop cycles and the clock (s_memrealtime = 100 MHz)
     const unsigned long long st_c1 = __builtin_amdgcn_s_memtime(), st_r1 = __builtin_amdgcn_s_memrealtime();
@@ -816,57 +840,90 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
 // Writes the skip s0 (B*48 x 128) and the pooled p0 (B*24 x 128).
 // ---------------------------------------------------------------------------
 template <typename T>
-__global__ __launch_bounds__(256) void down0_kernel(Down0Args a) {
-  __shared__ __attribute__((aligned(16))) float w[6 * 2 * 128];
+__global__ __launch_bounds__(512) void down0_kernel(Down0Args a, int spb) {
+  // One block per `spb` consecutive samples (<= 8).  The samples' x and the level's
+  // time + label map row block (t uniform, one condition) are staged in LDS once and
+  // each thread keeps its 8 channels' weights in registers, so the position loop
+  // only reads LDS operands and streams the s0 / p0 stores.
+  __shared__ __attribute__((aligned(16))) float mp[48 * 128];
+  __shared__ float xs[8 * 96];
+  __shared__ int uni;
   const int tid = threadIdx.x;
-  for (int i = tid; i < 6 * 2 * 128; i += 256) w[i] = a.w0[i];
-  __syncthreads();
-  const int pos = blockIdx.x * 16 + (tid >> 4);   // (sample, pooled position)
-  if (pos >= a.B * 24) return;
-  const int b = pos / 24, lp = pos - b * 24;
+  const int b0 = blockIdx.x * spb;
+  const int nb = min(spb, a.B - b0);
+  if (nb <= 0) return;
+  const int tac0 = a.tac ? a.tac[b0] : 0;
+  if (tid == 0) {
+    int u = a.t_uniform >= 0;
+    if (a.tac)
+      for (int k = 1; k < nb; ++k) u &= a.tac[b0 + k] == tac0;
+    uni = u;
+  }
+  for (int i = tid; i < nb * 96; i += 512) xs[i] = a.x[(size_t)b0 * 96 + i];
+  // this thread's 8 output channels: their 6 x 2 weights stay in registers
   const int n0 = (tid & 15) * 8;
-  const int l0 = 2 * lp;
-  const float* xb = a.x + (size_t)b * 96;
-  float xv[7][2];
+  f32x4 wr[12][2];
 #pragma unroll
-  for (int q = 0; q < 7; ++q) {
-    const int p = l0 - 2 + q;
-    const bool ok = (p >= 0 && p < 48);
-    xv[q][0] = ok ? xb[p * 2] : 0.f;
-    xv[q][1] = ok ? xb[p * 2 + 1] : 0.f;
+  for (int jc = 0; jc < 12; ++jc) {
+    wr[jc][0] = *reinterpret_cast<const f32x4*>(a.w0 + jc * 128 + n0);
+    wr[jc][1] = *reinterpret_cast<const f32x4*>(a.w0 + jc * 128 + n0 + 4);
   }
-  const int tac = a.tac ? a.tac[b] : 0;
-  const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[b];
-  float v[2][8];
+  __syncthreads();
+  const bool fast = uni != 0;
+  if (fast) {
+    const f32x4* tm = reinterpret_cast<const f32x4*>(a.tmap + (size_t)a.t_uniform * 48 * 128);
+    const f32x4* cm = reinterpret_cast<const f32x4*>(a.cmap + (size_t)tac0 * 48 * 128);
+    for (int i = tid; i < 48 * 128 / 4; i += 512) reinterpret_cast<f32x4*>(mp)[i] = tm[i] + cm[i];
+  }
+  __syncthreads();
+  for (int pos = tid >> 4; pos < nb * 24; pos += 32) {
+    const int bl = pos / 24, lp = pos - bl * 24, b = b0 + bl;
+    const int l0 = 2 * lp;
+    float xv[7][2];
 #pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const int l = l0 + e;
-    const float* tm = a.tmap + ((size_t)t * 48 + l) * 128 + n0;
-    const float* cm = a.cmap + ((size_t)tac * 48 + l) * 128 + n0;
-    f32x4 m0 = *reinterpret_cast<const f32x4*>(tm) + *reinterpret_cast<const f32x4*>(cm);
-    f32x4 m1 = *reinterpret_cast<const f32x4*>(tm + 4) + *reinterpret_cast<const f32x4*>(cm + 4);
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < 7; ++q) {
+      const int p = l0 - 2 + q;
+      const bool ok = (p >= 0 && p < 48);
+      xv[q][0] = ok ? xs[bl * 96 + p * 2] : 0.f;
+      xv[q][1] = ok ? xs[bl * 96 + p * 2 + 1] : 0.f;
+    }
+    float v[2][8];
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const f32x4 w0 = *reinterpret_cast<const f32x4*>(w + (j * 2 + c) * 128 + n0);
-        const f32x4 w1 = *reinterpret_cast<const f32x4*>(w + (j * 2 + c) * 128 + n0 + 4);
-        acc0 += w0 * xv[e + j][c];
-        acc1 += w1 * xv[e + j][c];
+    for (int e = 0; e < 2; ++e) {
+      const int l = l0 + e;
+      f32x4 m0, m1;
+      if (fast) {
+        m0 = *reinterpret_cast<const f32x4*>(mp + l * 128 + n0);
+        m1 = *reinterpret_cast<const f32x4*>(mp + l * 128 + n0 + 4);
+      } else {
+        const int tac = a.tac ? a.tac[b] : 0;
+        const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[b];
+        const float* tmr = a.tmap + ((size_t)t * 48 + l) * 128 + n0;
+        const float* cmr = a.cmap + ((size_t)tac * 48 + l) * 128 + n0;
+        m0 = *reinterpret_cast<const f32x4*>(tmr) + *reinterpret_cast<const f32x4*>(cmr);
+        m1 = *reinterpret_cast<const f32x4*>(tmr + 4) + *reinterpret_cast<const f32x4*>(cmr + 4);
       }
-    }
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      v[e][q] = fmaxf(acc0[q] + m0[q], 0.f);
-      v[e][4 + q] = fmaxf(acc1[q] + m1[q], 0.f);
+      for (int j = 0; j < 6; ++j) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          acc0 += wr[j * 2 + c][0] * xv[e + j][c];
+          acc1 += wr[j * 2 + c][1] * xv[e + j][c];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[e][q] = fmaxf(acc0[q] + m0[q], 0.f);
+        v[e][4 + q] = fmaxf(acc1[q] + m1[q], 0.f);
+      }
+      Vec8<T>::store(reinterpret_cast<T*>(a.s0) + ((size_t)b * 48 + l) * 128 + n0, v[e]);
     }
-    Vec8<T>::store(reinterpret_cast<T*>(a.s0) + ((size_t)b * 48 + l) * 128 + n0, v[e]);
+    float pv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) pv[q] = fmaxf(v[0][q], v[1][q]);
+    Vec8<T>::store(reinterpret_cast<T*>(a.p0) + ((size_t)b * 24 + lp) * 128 + n0, pv);
   }
-  float pv[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) pv[q] = fmaxf(v[0][q], v[1][q]);
-  Vec8<T>::store(reinterpret_cast<T*>(a.p0) + ((size_t)b * 24 + lp) * 128 + n0, pv);
 }
 
 // ---------------------------------------------------------------------------
@@ -1019,7 +1076,9 @@ hipError_t launch_conv(int kind, const ConvArgs<T>& a, hipStream_t s) {
 template <typename T>
 hipError_t launch_down0(const Down0Args& a, hipStream_t s) {
   if (a.B <= 0) return hipSuccess;
-  hipLaunchKernelGGL(down0_kernel<T>, dim3((a.B * 24 + 15) / 16), dim3(256), 0, s, a);
+  // ~1 block per CU: spb samples per block (<= 8, the LDS x stage)
+  const int spb = std::min(8, std::max(1, (a.B + 255) / 256));
+  hipLaunchKernelGGL(down0_kernel<T>, dim3((a.B + spb - 1) / spb), dim3(512), 0, s, a, spb);
   return hipGetLastError();
 }
 

@@ -4,6 +4,7 @@ TAG=${1:-run}
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/$TAG
+if [ -n "$MICRO" ]; then MODES="$MICRO" TAG=$TAG bash scripts/micro/run.sh > /dev/null || exit $?; fi
 timeout -k 10 600 python -m pytest tests -q -m gpu -p no:cacheprovider ${PYTEST_ARGS} > gpurun_out/$TAG/pytest.log 2>&1
 rc=$?
 echo "pytest exit $rc" >> gpurun_out/$TAG/pytest.log
