@@ -9,13 +9,23 @@
 // the MvNormal prior change is 2 d g_i + d^2 P_ii (g kept current on accept).
 #include "mh_internal.h"
 
+// Tuning knobs (the product uses the defaults; scripts/micro/build_mh.sh builds variants)
+#ifndef MH_EXP_MODE
+#define MH_EXP_MODE 0     // timing experiments only: bits drop exp / log / log_ndtr / sqrt / divisions
+#endif
+#ifndef MH_MV_UNROLL
+#define MH_MV_UNROLL 28   // operator-row matvec: 16-B steps unrolled
+#endif
+
 namespace petmh {
 
 constexpr int NR = kNRoi, NF = kNFrames;
 constexpr int kWaves = 8;             // chains per workgroup (512 threads)
 
+constexpr int MLD = 56;               // padded operator row (16-B aligned pairs)
+
 struct Lds {
-  double M[NF * NF];                  // SRTM2 operator, [g][f]
+  double M[NF * MLD];                 // SRTM2 operator, [f][g] (row per frame, g padded to 56)
   double PD[NR * NR], PR[NR * NR];    // prior precision matrices
   double Y[NR * NF], SIG[NR * NF];    // observed TAC / dt and noise sigma, [roi][frame]
   double CR[NF], TV[NF];
@@ -27,12 +37,37 @@ struct Lds {
   int ORD[kWaves][2 * NR];            //   the sweep's element order
 };
 
-// Butterfly sum; lanes may differ in the last bit (different pairing order), so the
-// result is broadcast from lane 0 to keep every accept/reject decision wave-uniform.
+// DPP move of a double (two 32-bit halves); lanes without a source read 0.
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, ROW_MASK, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROW_MASK, 0xf, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// Wave sum with DPP row shifts + row broadcasts (gfx9), total in lane 63, returned to
+// every lane through an SGPR (readlane): one wave-uniform value, so every accept /
+// reject decision is taken identically by all lanes.
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return __shfl(v, 0, 64);
+  v += dpp_f64<0x111>(v);          // row_shr:1
+  v += dpp_f64<0x112>(v);          // row_shr:2
+  v += dpp_f64<0x114>(v);          // row_shr:4
+  v += dpp_f64<0x118>(v);          // row_shr:8   -> lane 15 of each row: the row's sum
+  v += dpp_f64<0x142, 0xa>(v);     // row_bcast:15 into rows 1, 3
+  v += dpp_f64<0x143, 0xc>(v);     // row_bcast:31 into rows 2, 3 -> lane 63: total
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), 63);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// Value of a double held by lane `src` (wave-uniform index), as an SGPR broadcast.
+__device__ __forceinline__ double lane_bcast(double v, int src) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), src);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
 __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
@@ -57,26 +92,61 @@ __device__ __forceinline__ double log_ndtr(double x) {
 __device__ __forceinline__ double roi_loglik(const Lds& s, double* e, int lane, int i, double dvr, double r1, double k2p) {
   const double k2 = k2p * r1;           // kinetic_model.py:153-154
   const double k2a = k2 / dvr;
-  if (lane < NF) e[lane] = exp(-k2a * s.TV[lane]);
+#if MH_EXP_MODE & 1
+  e[lane] = lane < NF ? 1.0 - k2a * s.TV[lane < NF ? lane : 0] : 0.0;
+#else
+  e[lane] = lane < NF ? exp(-k2a * s.TV[lane < NF ? lane : 0]) : 0.0;   // e[54..63] = 0 (row padding)
+#endif
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   double l = 0.0;
   if (lane < NF) {
-    double conv = 0.0;
-#pragma unroll 6
-    for (int g = 0; g < NF; ++g) conv = fma(s.M[g * NF + lane], e[g], conv);
+    // conv_f = sum_g M[f][g] e[g]: own operator row, e broadcast, 16-B reads, 2 chains
+    const double2* mrow = reinterpret_cast<const double2*>(s.M + lane * MLD);
+    const double2* ev = reinterpret_cast<const double2*>(e);
+    double c0 = 0.0, c1 = 0.0;
+#pragma unroll MH_MV_UNROLL
+    for (int q = 0; q < MLD / 2; ++q) {
+      const double2 m = mrow[q], x = ev[q];
+      c0 = fma(m.x, x.x, c0);
+      c1 = fma(m.y, x.y, c1);
+    }
+    const double conv = c0 + c1;
     const double tac = r1 * s.CR[lane] + (k2 - r1 * k2a) * conv;   // :157-158
     const double sn = tac < 0.0 ? 1e-6 : tac;                       // mcmc.py:152
+#if MH_EXP_MODE & 8
+    const double sig = sn * s.SIG[i * NF + lane];
+#else
     const double sig = sqrt(sn) * s.SIG[i * NF + lane];             // :153
-    const double z = (s.Y[i * NF + lane] - sn) / sig;
-    l = -0.5 * z * z - 0.9189385332046727 - log(sig) - log_ndtr(sn / sig);
+#endif
+#if MH_EXP_MODE & 16
+    const double inv = sig;
+#else
+    const double inv = 1.0 / sig;
+#endif
+    const double z = (s.Y[i * NF + lane] - sn) * inv;
+    const double xs = sn * inv;
+    // log Phi(x) for x >= 10 is -7.6e-24 or smaller: 0 at the precision of the sum
+#if MH_EXP_MODE & 4
+    const double lnd = 0.0;
+#else
+    const double lnd = xs < 10.0 ? log_ndtr(xs) : 0.0;
+#endif
+#if MH_EXP_MODE & 2
+    l = -0.5 * z * z - 0.9189385332046727 - sig - lnd;
+#else
+    l = -0.5 * z * z - 0.9189385332046727 - log(sig) - lnd;
+#endif
   }
   __builtin_amdgcn_wave_barrier();
   return wave_sum(l);
 }
 
 __device__ void load_lds(Lds& s, const MHConst& c) {
-  for (int k = threadIdx.x; k < NF * NF; k += blockDim.x) s.M[k] = c.M[k];
+  for (int k = threadIdx.x; k < NF * MLD; k += blockDim.x) {
+    const int f = k / MLD, g = k - f * MLD;
+    s.M[k] = g < NF ? c.M[g * NF + f] : 0.0;   // global operator is [g][f]
+  }
   for (int k = threadIdx.x; k < NR * NR; k += blockDim.x) { s.PD[k] = c.PD[k]; s.PR[k] = c.PR[k]; }
   for (int k = threadIdx.x; k < NR * NF; k += blockDim.x) { s.Y[k] = c.Y[k]; s.SIG[k] = c.SIG[k]; }
   for (int k = threadIdx.x; k < NF; k += blockDim.x) { s.CR[k] = c.CR[k]; s.TV[k] = c.TV[k]; }
@@ -133,7 +203,7 @@ __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun 
     double ll = 0.0;
 #pragma unroll 1
     for (int i = 0; i < NR; ++i) {
-      const double di = __shfl(D, i, 64), ri = __shfl(R, i, 64);
+      const double di = lane_bcast(D, i), ri = lane_bcast(R, i);
       const double v = roi_loglik(s, e, lane, i, di, ri, c.k2p);
       if (lane == i) ll = v;
     }
@@ -187,14 +257,14 @@ __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun 
       double run = 0.0;                  // log p(running) - log p(sweep start)
 #pragma unroll 1
       for (int j = 0; j < 2 * NR; ++j) {
-        const int k = ORDw[j];
+        const int k = __builtin_amdgcn_readfirstlane(ORDw[j]);
         const int v = k >= NR, i = v ? k - NR : k;
         const double* P = v ? s.PR : s.PD;
-        const double Di = __shfl(D, i, 64), Ri = __shfl(R, i, 64);
+        const double Di = lane_bcast(D, i), Ri = lane_bcast(R, i);
         const double xi = v ? Ri : Di;
-        const double si = __shfl(v ? sR : sD, i, 64);
-        const double gi = __shfl(v ? gR : gD, i, 64);
-        const double lli = __shfl(ll, i, 64);
+        const double si = v ? lane_bcast(sR, i) : lane_bcast(sD, i);
+        const double gi = v ? lane_bcast(gR, i) : lane_bcast(gD, i);
+        const double lli = lane_bcast(ll, i);
         const double delta = Zw[k] * si;
         const double xp = xi + delta;
         const double dprior = -0.5 * (2.0 * delta * gi + delta * delta * P[i * NR + i]);
@@ -255,7 +325,7 @@ __global__ __launch_bounds__(kWaves * 64) void mh_logp_kernel(MHConst c, const d
   for (int pt = blockIdx.x * kWaves + w; pt < n; pt += gridDim.x * kWaves) {
     const double D = x[(size_t)pt * 2 * NR + li], R = x[(size_t)pt * 2 * NR + NR + li];
     double ll = 0.0;
-    for (int i = 0; i < NR; ++i) ll += roi_loglik(s, e, lane, i, __shfl(D, i, 64), __shfl(R, i, 64), c.k2p);
+    for (int i = 0; i < NR; ++i) ll += roi_loglik(s, e, lane, i, lane_bcast(D, i), lane_bcast(R, i), c.k2p);
     // MvNormal quadratic forms
     double q = 0.0;
     for (int v = 0; v < 2; ++v) {

@@ -847,20 +847,14 @@ __global__ __launch_bounds__(512) void down0_kernel(Down0Args a, int spb) {
   // only reads LDS operands and streams the s0 / p0 stores.
   __shared__ __attribute__((aligned(16))) float mp[48 * 128];
   __shared__ float xs[8 * 96];
-  __shared__ int uni;
   const int tid = threadIdx.x;
   const int b0 = blockIdx.x * spb;
   const int nb = min(spb, a.B - b0);
   if (nb <= 0) return;
+  // every global load is issued before the single barrier, so their latencies overlap
   const int tac0 = a.tac ? a.tac[b0] : 0;
-  if (tid == 0) {
-    int u = a.t_uniform >= 0;
-    if (a.tac)
-      for (int k = 1; k < nb; ++k) u &= a.tac[b0 + k] == tac0;
-    uni = u;
-  }
-  for (int i = tid; i < nb * 96; i += 512) xs[i] = a.x[(size_t)b0 * 96 + i];
-  // this thread's 8 output channels: their 6 x 2 weights stay in registers
+  bool fast = a.t_uniform >= 0;                   // t uniform and one condition in the block
+  if (a.tac) fast = __syncthreads_and(fast && (tid >= nb || a.tac[b0 + tid] == tac0)) != 0;
   const int n0 = (tid & 15) * 8;
   f32x4 wr[12][2];
 #pragma unroll
@@ -868,12 +862,20 @@ __global__ __launch_bounds__(512) void down0_kernel(Down0Args a, int spb) {
     wr[jc][0] = *reinterpret_cast<const f32x4*>(a.w0 + jc * 128 + n0);
     wr[jc][1] = *reinterpret_cast<const f32x4*>(a.w0 + jc * 128 + n0 + 4);
   }
-  __syncthreads();
-  const bool fast = uni != 0;
+  const float xin = tid < nb * 96 ? a.x[(size_t)b0 * 96 + tid] : 0.f;   // nb * 96 <= 768: two passes
+  const float xin2 = tid + 512 < nb * 96 ? a.x[(size_t)b0 * 96 + tid + 512] : 0.f;
+  f32x4 mv[3];
   if (fast) {
     const f32x4* tm = reinterpret_cast<const f32x4*>(a.tmap + (size_t)a.t_uniform * 48 * 128);
     const f32x4* cm = reinterpret_cast<const f32x4*>(a.cmap + (size_t)tac0 * 48 * 128);
-    for (int i = tid; i < 48 * 128 / 4; i += 512) reinterpret_cast<f32x4*>(mp)[i] = tm[i] + cm[i];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) mv[k] = tm[tid + 512 * k] + cm[tid + 512 * k];
+  }
+  if (tid < nb * 96) xs[tid] = xin;
+  if (tid + 512 < nb * 96) xs[tid + 512] = xin2;
+  if (fast) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) reinterpret_cast<f32x4*>(mp)[tid + 512 * k] = mv[k];
   }
   __syncthreads();
   for (int pos = tid >> 4; pos < nb * 24; pos += 32) {
