@@ -41,7 +41,7 @@ def parse():
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--batch', type=int, default=1024, help='posterior samples per GPU')
     ap.add_argument('--reverse-steps', type=int, default=1000)
-    ap.add_argument('--dtype', default='bfloat16', choices=['bfloat16', 'float32'])
+    ap.add_argument('--dtype', default='bfloat16', choices=['bfloat16', 'float16', 'float32'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-kernel-timing', action='store_true')
     ap.add_argument('--workload', default='iddpm', choices=['iddpm', 'mh'],
@@ -276,7 +276,7 @@ def main():
         samples = world * B * args.steps
         value = samples / elapsed
         tflops_pipeline = FLOP_PER_SAMPLE_STEP * n_rev * samples / elapsed / 1e12
-        peak = PEAK_BF16_TFLOPS if args.dtype == 'bfloat16' else PEAK_F32_TFLOPS
+        peak = PEAK_F32_TFLOPS if args.dtype == 'float32' else PEAK_BF16_TFLOPS   # fp16 dense = bf16 dense
         roof = None
         if layer_ms is not None:
             ms, cnt = layer_ms['up0.block']
@@ -292,7 +292,7 @@ def main():
             'metric': 'posterior samples/sec (48-ROI TAC, 1000-step reverse) at 1/2/4/8 MI355X',
             'value': round(value, 2), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True,
-            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16' if args.dtype == 'bfloat16' else 'f32',
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': {'bfloat16': 'bf16', 'float16': 'f16', 'float32': 'f32'}[args.dtype],
             'data': 'synthetic (SRTM2 TACs + noise model; identity-denoiser Glorot weights of the shipped net)',
             'config': {'workload': 'iDDPM reverse process, f128/d4 1-D conditional U-Net, 48-ROI x 2 params',
                        'n_posterior_per_gpu': B, 'reverse_steps': n_rev, 'global_batch': world * B,

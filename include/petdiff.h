@@ -57,6 +57,7 @@ extern "C" {
 
 #define PETDIFF_DTYPE_F32 0        /* exact-f32 MFMA network (parity mode)    */
 #define PETDIFF_DTYPE_BF16 1       /* bf16 MFMA network, fp32 accumulate + fp32 p_sample */
+#define PETDIFF_DTYPE_F16 2        /* fp16 MFMA network (BASELINE config 5), fp32 accumulate + p_sample */
 
 #define PETDIFF_LEARN_FIXED 0      /* learn_variance = ''            */
 #define PETDIFF_LEARN 1            /* 'learn'                         */

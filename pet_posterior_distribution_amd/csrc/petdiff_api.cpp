@@ -9,6 +9,7 @@
 
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 #include <map>
 #include <memory>
 #include <string>
@@ -43,6 +44,13 @@ uint16_t f2bf(float f) {
   std::memcpy(&u, &f, 4);
   u += 0x7FFFu + ((u >> 16) & 1u);
   return (uint16_t)(u >> 16);
+}
+
+uint16_t f2h(float f) {   // IEEE binary16, round to nearest even (compiler conversion)
+  const _Float16 h = (_Float16)f;
+  uint16_t u;
+  std::memcpy(&u, &h, 2);
+  return u;
 }
 
 struct Spec {
@@ -210,7 +218,7 @@ struct petdiff_ctx {
   size_t ev_next = 0;
 
   const float* W(const std::string& n) const { return w32.as<float>() + off.at(n); }
-  size_t act_bytes() const { return cfg.dtype == PETDIFF_DTYPE_BF16 ? 2 : 4; }
+  size_t act_bytes() const { return cfg.dtype == PETDIFF_DTYPE_F32 ? 4 : 2; }
 };
 
 namespace {
@@ -251,7 +259,8 @@ int pack_conv(petdiff_ctx* h, const std::vector<float>& wk_host, int li) {
               const int co = nt * NT + n;
               float v = wk[((size_t)j * cl.cin_full + ci) * cl.cout + co];
               if (wr && j == cl.padl) v += wr[(size_t)ci * cl.cout + co];
-              if constexpr (sizeof(H) == 2) out[q++] = f2bf(v);
+              if constexpr (std::is_same<T, f16>::value) out[q++] = f2h(v);
+              else if constexpr (sizeof(H) == 2) out[q++] = f2bf(v);
               else out[q++] = v;
             }
           }
@@ -384,6 +393,7 @@ int network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
   if (!h->sched_set) return fail(PETDIFF_ERR_INVALID, "schedule not set (petdiff_set_schedule)");
   if (h->n_tac <= 0) return fail(PETDIFF_ERR_INVALID, "conditions not set (petdiff_set_conditions)");
   if (h->cfg.dtype == PETDIFF_DTYPE_BF16) return run_network<bf16>(h, io, B, s);
+  if (h->cfg.dtype == PETDIFF_DTYPE_F16) return run_network<f16>(h, io, B, s);
   return run_network<float>(h, io, B, s);
 }
 
@@ -461,8 +471,8 @@ int petdiff_create(const petdiff_config* cfg, const float* weights, size_t n_wei
   if (!is_shipped_arch(*cfg))
     return fail(PETDIFF_ERR_UNSUPPORTED,
                 "only the shipped UnetConditional (f128/d4, k6, L48, enc 256-128-64-32) is compiled");
-  if (cfg->dtype != PETDIFF_DTYPE_F32 && cfg->dtype != PETDIFF_DTYPE_BF16)
-    return fail(PETDIFF_ERR_INVALID, "dtype must be PETDIFF_DTYPE_F32 or PETDIFF_DTYPE_BF16");
+  if (cfg->dtype != PETDIFF_DTYPE_F32 && cfg->dtype != PETDIFF_DTYPE_BF16 && cfg->dtype != PETDIFF_DTYPE_F16)
+    return fail(PETDIFF_ERR_INVALID, "dtype must be PETDIFF_DTYPE_F32, PETDIFF_DTYPE_BF16 or PETDIFF_DTYPE_F16");
   if (cfg->learn_variance < 0 || cfg->learn_variance > 2 || cfg->parameterization < 0 ||
       cfg->parameterization > 3)
     return fail(PETDIFF_ERR_INVALID, "bad learn_variance / parameterization");
@@ -483,6 +493,7 @@ int petdiff_create(const petdiff_config* cfg, const float* weights, size_t n_wei
   std::vector<float> host(weights, weights + need);
   for (int li = 0; li < kNumConvLayers; ++li) {
     if (cfg->dtype == PETDIFF_DTYPE_BF16) CHK((pack_conv<bf16, uint16_t>(h.get(), host, li)));
+    else if (cfg->dtype == PETDIFF_DTYPE_F16) CHK((pack_conv<f16, uint16_t>(h.get(), host, li)));
     else CHK((pack_conv<float, float>(h.get(), host, li)));
     const ConvLayer& cl = kConv[li];
     if (cl.cond_level < 0) {

@@ -8,6 +8,7 @@
 namespace petdiff {
 
 typedef __bf16 bf16;
+typedef _Float16 f16;
 
 // Tile geometry of the implicit-GEMM Conv1D kernel (see DESIGN.md "conv kernel").
 constexpr int kThreads = 256; // 4 waves; every wave owns a 96 x 64 output block (3 x 2 MFMA 32x32)

@@ -34,15 +34,31 @@
 namespace petdiff {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// 16-bit element types: MFMA operand fragment (8 elements per lane) and the
+// 32x32x16 MFMA of that type (bf16 default; fp16 for BASELINE config 5).
+template <typename T> struct Frag;
+template <> struct Frag<bf16> { typedef bf16x8 type; };
+template <> struct Frag<f16> { typedef f16x8 type; };
+template <> struct Frag<float> { typedef bf16x8 type; };   // unused by the f32 path
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 mfma32(f16x8 a, f16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 
 __device__ __forceinline__ float to_f(float v) { return v; }
 __device__ __forceinline__ float to_f(bf16 v) { return (float)v; }
+__device__ __forceinline__ float to_f(f16 v) { return (float)v; }
 template <typename T> __device__ __forceinline__ T from_f(float v);
 template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
 template <> __device__ __forceinline__ bf16 from_f<bf16>(float v) { return (bf16)v; }
+template <> __device__ __forceinline__ f16 from_f<f16>(float v) { return (f16)v; }
 
 // ---------------------------------------------------------------------------
 // Counter-based RNG: Philox4x32-10 + Box-Muller (restated in oracle/iddpm_ref.py)
@@ -297,6 +313,14 @@ template <> struct Vec8<bf16> {
     *reinterpret_cast<bf16x8*>(p) = o;
   }
 };
+template <> struct Vec8<f16> {
+  static __device__ __forceinline__ void store(f16* p, const float* v) {
+    f16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (f16)v[e];
+    *reinterpret_cast<f16x8*>(p) = o;
+  }
+};
 template <> struct Vec8<float> {
   static __device__ __forceinline__ void store(float* p, const float* v) {
     *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
@@ -403,16 +427,17 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
   // Within a step the reads and the DMA issue are interleaved one per MFMA gap
   // (sched_group_barrier: M R M R M R M R M R M V), so no gap carries more than one
   // ds_read_b128 (MI355X_MICROARCH.md LDS: a third read per gap saturates the array).
-  bf16x8 av[2][3], bv[2][2];
+  typedef typename Frag<T>::type fragT;
+  fragT av[2][3], bv[2][2];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) av[1][i] = av[0][i] = bf16x8{};
+  for (int i = 0; i < 3; ++i) av[1][i] = av[0][i] = fragT{};
 #pragma unroll
-  for (int jn = 0; jn < 2; ++jn) bv[1][jn] = bv[0][jn] = bf16x8{};
+  for (int jn = 0; jn < 2; ++jn) bv[1][jn] = bv[0][jn] = fragT{};
   if constexpr ((CONV_EXP_MODE & 64) != 0) {   // diagnostic: non-zero register operands
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      av[0][0][e] = av[1][1][e] = av[0][2][e] = (bf16)(0.01f * (lane + e));
-      bv[0][1][e] = bv[1][0][e] = (bf16)(0.02f * (lane - e));
+      av[0][0][e] = av[1][1][e] = av[0][2][e] = (decltype(av[0][0][0]))(0.01f * (lane + e));
+      bv[0][1][e] = bv[1][0][e] = (decltype(bv[0][0][0]))(0.02f * (lane - e));
     }
   }
   auto mfma_bf16 = [&](int pb) {
@@ -421,7 +446,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
 #pragma unroll
       for (int jn = 0; jn < 2; ++jn)
         if constexpr (sizeof(T) == 2 && !(CONV_EXP_MODE & 2))
-          acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[pb][i], bv[pb][jn], acc[i][jn], 0, 0, 0);
+          acc[i][jn] = mfma32(av[pb][i], bv[pb][jn], acc[i][jn]);
   };
   // NEXT = 2 (first chunk only): the pieces of chunks nkc and nkc + 1 (stages nbuf, nbuf + 1).
   auto compute = [&](const char* base, auto next_tag, int nkc, int nbuf) {
@@ -446,9 +471,9 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
         const int pb = sb ^ 1;
 #define PETDIFF_MF(i, jn)                                                                                  \
   if constexpr (!(CONV_EXP_MODE & 2))                                                                      \
-    acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[pb][i], bv[pb][jn], acc[i][jn], 0, 0, 0);
+    acc[i][jn] = mfma32(av[pb][i], bv[pb][jn], acc[i][jn]);
 #define PETDIFF_RD(dst, ptr) \
-  if constexpr (!(CONV_EXP_MODE & 64)) dst = *reinterpret_cast<const bf16x8*>(ptr);
+  if constexpr (!(CONV_EXP_MODE & 64)) dst = *reinterpret_cast<const fragT*>(ptr);
         PETDIFF_MF(0, 0)
         PETDIFF_RD(av[sb][0], pa0)
         __builtin_amdgcn_sched_barrier(0);
@@ -1085,8 +1110,10 @@ hipError_t launch_down0(const Down0Args& a, hipStream_t s) {
 }
 
 template hipError_t launch_conv<bf16>(int, const ConvArgs<bf16>&, hipStream_t);
+template hipError_t launch_conv<f16>(int, const ConvArgs<f16>&, hipStream_t);
 template hipError_t launch_conv<float>(int, const ConvArgs<float>&, hipStream_t);
 template hipError_t launch_down0<bf16>(const Down0Args&, hipStream_t);
+template hipError_t launch_down0<f16>(const Down0Args&, hipStream_t);
 template hipError_t launch_down0<float>(const Down0Args&, hipStream_t);
 
 hipError_t launch_time_emb(const float* w, const float* b, int T, int sin_dim, int hid, float* out,

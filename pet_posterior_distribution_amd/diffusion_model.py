@@ -117,6 +117,7 @@ class ImprovedDDPM:
         self.posterior_mean_coef2 = (1.0 - self.alpha_bar_prev) * np.sqrt(self.alpha) / (1.0 - self.alpha_bar)
 
         self.dtype = {'bfloat16': _lib.DTYPE_BF16, 'bf16': _lib.DTYPE_BF16,
+                      'float16': _lib.DTYPE_F16, 'fp16': _lib.DTYPE_F16, 'half': _lib.DTYPE_F16,
                       'float32': _lib.DTYPE_F32, 'fp32': _lib.DTYPE_F32}[str(dtype)]
         if device is None:
             device = torch.cuda.current_device() if torch.cuda.is_available() else 0

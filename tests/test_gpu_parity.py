@@ -3,6 +3,7 @@
 Tolerances (written per test):
 * exact-f32 MFMA network: max|gpu - oracle_fp64| <= 1e-4 * max|oracle| (north_star: 1e-4 rtol);
 * bf16 network (fp32 accumulate): <= 3e-2 * max|oracle| on one forward;
+* fp16 network (fp32 accumulate, BASELINE config 5): <= 5e-3 * max|oracle| on one forward;
 * p_sample / loop with identical injected noise: posterior mean / SD within 1e-4 rtol.
 """
 import numpy as np
@@ -58,6 +59,34 @@ def test_unet_forward_f32(m32, conds):
     ref = R.unet_forward(m32.network.weights, x, t, cond, dt=np.float64)
     assert out.shape == (B, 48, 4)
     assert rel(out, ref) < 1e-4
+
+
+@pytest.fixture(scope='module')
+def mh16():
+    return make_model('float16')
+
+
+def test_unet_forward_fp16(mh16, conds):
+    rng = np.random.default_rng(3)
+    B = 8
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    t = np.array([999, 700, 500, 250, 17, 2, 1, 0], dtype=np.int32)
+    cond = conds[np.array([0, 1, 1, 0, 0, 1, 0, 1])]
+    out = mh16.call({'x': x, 'time': t, 'condition': cond})
+    ref = R.unet_forward(mh16.network.weights, x, t, cond, dt=np.float64)
+    assert rel(out, ref) < 5e-3
+
+
+def test_fp16_loop_statistics_vs_f32(mh16, m32, conds):
+    """fp16 network vs exact-f32 network on the same counter-based noise (100-step loop)."""
+    rng = np.random.default_rng(12)
+    B = 256
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    a = mh16.ddpm_loop(x, conds[:1], num_timesteps=100, seed=5).cpu().numpy()
+    b = m32.ddpm_loop(x, conds[:1], num_timesteps=100, seed=5).cpu().numpy()
+    assert np.isfinite(a).all()
+    scale = np.abs(b).mean()
+    assert np.abs(a.mean(0) - b.mean(0)).max() < 0.05 * scale
 
 
 def test_unet_forward_bf16(m16, conds):
