@@ -71,6 +71,11 @@ int petmh_destroy(petmh_handle h);
 int petmh_run(petmh_handle h, const double* x0_dev, int n_chains, int n_draws, int n_tune, uint64_t seed,
               double* stats_dev, double* accept_dev, double* last_dev, void* stream);
 
+/* petmh_run that also writes the kept draws (the reference's idata trace,
+ * mcmc.py:157-165): draws_dev [n_chains][n_draws][2*n_roi] fp64 (DVR | R1). */
+int petmh_run_draws(petmh_handle h, const double* x0_dev, int n_chains, int n_draws, int n_tune, uint64_t seed,
+                    double* stats_dev, double* accept_dev, double* last_dev, double* draws_dev, void* stream);
+
 /* Sampler options (defaults = pymc Metropolis: tune_interval 100, scaling 1.0,
  * vs_sweep_start 1).  vs_sweep_start 0 compares each element against the running
  * state instead (textbook component-wise MH). */

@@ -63,8 +63,15 @@ SYMBOLS = [
     ('petmh_run', C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_p, C.c_void_p,
                             C.c_void_p, C.c_void_p]),
     ('petmh_set_sampler', C.c_int, [C.c_void_p, C.c_int, C.c_double, C.c_int]),
+    ('petmh_run_draws', C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_p,
+                                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     ('petmh_logp', C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
     ('petmh_last_error', C.c_char_p, []),
+    # posterior accuracy metrics (include/petmetrics.h)
+    ('petmetrics_moments', C.c_int, [C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                     C.c_void_p, C.c_void_p]),
+    ('petmetrics_work_doubles', C.c_size_t, [C.c_int]),
+    ('petmetrics_last_error', C.c_char_p, []),
 ]
 
 

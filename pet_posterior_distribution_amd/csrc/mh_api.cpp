@@ -214,6 +214,11 @@ int petmh_destroy(petmh_handle h) {
 
 int petmh_run(petmh_handle h, const double* x0, int n_chains, int n_draws, int n_tune, uint64_t seed, double* stats,
               double* accept, double* last, void* stream) {
+  return petmh_run_draws(h, x0, n_chains, n_draws, n_tune, seed, stats, accept, last, nullptr, stream);
+}
+
+int petmh_run_draws(petmh_handle h, const double* x0, int n_chains, int n_draws, int n_tune, uint64_t seed,
+                    double* stats, double* accept, double* last, double* draws, void* stream) {
   if (!h || !stats || n_chains < 0 || n_draws < 0 || n_tune < 0) return fail("bad arguments");
   HIPC(hipSetDevice(h->device));
   MHRun r{};
@@ -228,6 +233,7 @@ int petmh_run(petmh_handle h, const double* x0, int n_chains, int n_draws, int n
   r.stats = stats;
   r.accept = accept;
   r.last = last;
+  r.draws = draws;
   HIPC(launch_mh_chains(h->c, r, (hipStream_t)stream));
   return 0;
 }

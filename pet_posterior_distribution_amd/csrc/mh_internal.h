@@ -32,6 +32,7 @@ struct MHRun {
   double* stats;               // [n_chains][96][3]
   double* accept;              // [n_chains][96] or null
   double* last;                // [n_chains][96] or null
+  double* draws;               // [n_chains][n_draws][96] or null (kept draws)
 };
 
 hipError_t launch_mh_chains(const MHConst& c, const MHRun& r, hipStream_t s);

@@ -286,6 +286,11 @@ __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun 
       }
       __builtin_amdgcn_wave_barrier();
       if (it >= r.n_tune) {              // Welford over kept draws
+        if (r.draws && own) {            // optional trace [chain][draw][DVR 48 | R1 48] (mcmc.py idata)
+          double* dr = r.draws + ((size_t)chain * r.n_draws + (it - r.n_tune)) * 2 * NR;
+          dr[lane] = D;
+          dr[NR + lane] = R;
+        }
         ++nk;
         const double dd = D - mD;
         mD += dd / (double)nk;

@@ -64,8 +64,10 @@ class MetropolisSRTM2:
                                             C.c_void_p(out.data_ptr()), self._stream()), 'petmh_logp')
         return out
 
-    def run(self, n_chains, draws, tune, seed=0, x0=None, return_chains=False):
-        """pm.sample(draws, tune, step=Metropolis(NormalProposal)) (mcmc.py:156-157) over n_chains chains."""
+    def run(self, n_chains, draws, tune, seed=0, x0=None, return_chains=False, return_draws=False):
+        """pm.sample(draws, tune, step=Metropolis(NormalProposal)) (mcmc.py:156-157) over n_chains chains.
+        return_draws: also keep the trace (the reference's idata, mcmc.py:162-164) as
+        res['draws'], a CUDA fp64 tensor (n_chains, draws, 96) = [DVR | R1]."""
         x0t = None if x0 is None else torch.as_tensor(np.asarray(x0), dtype=torch.float64,
                                                        device=self.device).reshape(n_chains, 96).contiguous()
         stats = torch.empty((n_chains, 96, 3), dtype=torch.float64, device=self.device)
@@ -73,10 +75,13 @@ class MetropolisSRTM2:
         last = torch.empty((n_chains, 96), dtype=torch.float64, device=self.device)
         torch.cuda.synchronize(self.device)
         t0 = time.perf_counter()
-        _lib.check_mh(_lib.lib().petmh_run(self._h, None if x0t is None else C.c_void_p(x0t.data_ptr()), n_chains,
-                                           draws, tune, int(seed), C.c_void_p(stats.data_ptr()),
-                                           C.c_void_p(acc.data_ptr()), C.c_void_p(last.data_ptr()),
-                                           self._stream()), 'petmh_run')
+        trace = (torch.empty((n_chains, draws, 96), dtype=torch.float64, device=self.device)
+                 if return_draws else None)
+        _lib.check_mh(_lib.lib().petmh_run_draws(self._h, None if x0t is None else C.c_void_p(x0t.data_ptr()),
+                                                 n_chains, draws, tune, int(seed), C.c_void_p(stats.data_ptr()),
+                                                 C.c_void_p(acc.data_ptr()), C.c_void_p(last.data_ptr()),
+                                                 None if trace is None else C.c_void_p(trace.data_ptr()),
+                                                 self._stream()), 'petmh_run')
         torch.cuda.synchronize(self.device)
         elapsed = time.perf_counter() - t0
         st = stats.cpu().numpy()
@@ -85,6 +90,8 @@ class MetropolisSRTM2:
         res = {'mean_DVR': mean[:48], 'mean_R1': mean[48:], 'std_DVR': std[:48], 'std_R1': std[48:],
                'accept_rate': acc.cpu().numpy() / max(draws, 1), 'elapsed_s': elapsed,
                'chain_draws_per_s': n_chains * (draws + tune) / elapsed if elapsed > 0 else float('inf')}
+        if return_draws:
+            res['draws'] = trace
         if return_chains:
             res['chain_stats'] = st
             res['last'] = last.cpu().numpy()

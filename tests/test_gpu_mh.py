@@ -117,3 +117,18 @@ def test_mh_chains_match_c_oracle(g2, vs0):
     np.testing.assert_allclose(res['chain_stats'][same][..., 1], st[same][..., 1], rtol=1e-9)
     np.testing.assert_allclose(res['chain_stats'][same][..., 2], st[same][..., 2], rtol=1e-6, atol=1e-12)
     mh.close()
+
+
+def test_mh_trace_matches_welford(g2):
+    """petmh_run_draws: the stored trace reproduces the on-GPU Welford moments."""
+    from pet_posterior_distribution_amd.mcmc import MetropolisSRTM2
+    P = make_problem(g2, case=1)
+    mh = MetropolisSRTM2(**P)
+    res = mh.run(16, 40, 30, seed=5, return_chains=True, return_draws=True)
+    tr = res['draws'].cpu().numpy()
+    assert tr.shape == (16, 40, 96)
+    np.testing.assert_allclose(res['chain_stats'][..., 1], tr.mean(1), rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(res['chain_stats'][..., 2], ((tr - tr.mean(1, keepdims=True)) ** 2).sum(1),
+                               rtol=1e-9, atol=1e-14)
+    np.testing.assert_array_equal(res['last'], tr[:, -1])
+    mh.close()
