@@ -20,7 +20,10 @@
 namespace petmh {
 
 constexpr int NR = kNRoi, NF = kNFrames;
-constexpr int kWaves = 8;             // chains per workgroup (512 threads)
+#ifndef MH_WAVES
+#define MH_WAVES 8
+#endif
+constexpr int kWaves = MH_WAVES;      // chains per workgroup (64 * kWaves threads)
 
 constexpr int MLD = 56;               // padded operator row (16-B aligned pairs)
 
