@@ -40,6 +40,8 @@ def parse():
     ap.add_argument('--steps', type=int, default=3)
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--batch', type=int, default=1024, help='posterior samples per GPU')
+    ap.add_argument('--tacs', type=int, default=1,
+                    help='test TACs per GPU (samples split TAC-major; config 4 = 32 TACs x 8192 per GPU)')
     ap.add_argument('--reverse-steps', type=int, default=1000)
     ap.add_argument('--dtype', default='bfloat16', choices=['bfloat16', 'float16', 'float32'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -219,7 +221,12 @@ def main():
     net.build((None, 48, 2))
     model = ImprovedDDPM(network=net, dtype=args.dtype, device=dev.index, **shipped_diff_args())
     B = args.batch
-    cond = make_condition(seed=rank)                  # one synthetic test TAC per rank
+    n_tac = args.tacs
+    if n_tac < 1 or B % n_tac:
+        raise SystemExit('--batch must be a multiple of --tacs')
+    # the rank's synthetic test TACs (global TAC index rank * n_tac + k), samples TAC-major
+    cond = np.stack([make_condition(seed=rank * n_tac + k) for k in range(n_tac)])
+    tac = torch.arange(n_tac, device=dev, dtype=torch.int32).repeat_interleave(B // n_tac)
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
     x_T = torch.randn((B, 48, 2), generator=g, device=dev, dtype=torch.float32)
@@ -227,7 +234,8 @@ def main():
     offset = rank * B
 
     def one():
-        return model.ddpm_loop(x_T, cond[None], num_timesteps=n_rev, seed=2, sample_offset=offset)
+        return model.ddpm_loop(x_T, cond, num_timesteps=n_rev, seed=2, sample_offset=offset,
+                               tac=tac if n_tac > 1 else None)
 
     for _ in range(args.warmup):
         out = one()
@@ -249,7 +257,7 @@ def main():
         elapsed = float(e.item())
 
     # posterior summary: per-rank Welford partials, RCCL all-gather
-    st = model.posterior_stats(out)                               # (1, 48, 2, 3) fp64
+    st = model.posterior_stats(out, tac=tac if n_tac > 1 else None, n_tac=n_tac)   # (n_tac, 48, 2, 3) fp64
     st_t = torch.as_tensor(st, device=dev)
     ag_ms = 0.0
     if world > 1:
@@ -268,7 +276,8 @@ def main():
     layer_ms = None
     if not args.no_kernel_timing:
         model.set_kernel_timing(True)
-        model.ddpm_loop(x_T, cond[None], num_timesteps=n_rev, seed=2, sample_offset=offset, use_graph=False)
+        model.ddpm_loop(x_T, cond, num_timesteps=n_rev, seed=2, sample_offset=offset, use_graph=False,
+                        tac=tac if n_tac > 1 else None)
         layer_ms = model.get_kernel_timing()
         model.set_kernel_timing(False)
 
@@ -296,7 +305,7 @@ def main():
             'data': 'synthetic (SRTM2 TACs + noise model; identity-denoiser Glorot weights of the shipped net)',
             'config': {'workload': 'iDDPM reverse process, f128/d4 1-D conditional U-Net, 48-ROI x 2 params',
                        'n_posterior_per_gpu': B, 'reverse_steps': n_rev, 'global_batch': world * B,
-                       'tacs': world, 'parallelism': f'dp{world} (sample shards, RCCL all-gather of stats)',
+                       'tacs': world * n_tac, 'parallelism': f'dp{world} (sample shards, RCCL all-gather of stats)',
                        'hipgraph': True},
             'roofline': roof,
             'outputs_finite': finite,
@@ -305,7 +314,7 @@ def main():
         if layer_ms is not None:
             line['layer_us'] = {k: round(v[0] / max(v[1], 1) * 1e3, 2) for k, v in layer_ms.items()}
         if world == 1 and not args.no_cpu_baseline:
-            line['cpu_baseline'] = cpu_baseline(net.weights, cond)
+            line['cpu_baseline'] = cpu_baseline(net.weights, cond[0])
         else:
             line['cpu_baseline'] = None
         sm = allst[..., 1]
