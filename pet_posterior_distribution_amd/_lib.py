@@ -11,7 +11,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libpetdiff.so')
+# PETDIFF_LIB: an alternative build of the same library (A/B timing of kernel variants)
+LIB_PATH = os.environ.get('PETDIFF_LIB') or os.path.join(_HERE, 'libpetdiff.so')
 
 PETDIFF_OK, PETDIFF_ERR_INVALID, PETDIFF_ERR_HIP, PETDIFF_ERR_UNSUPPORTED = 0, 1, 2, 3
 DTYPE_F32, DTYPE_BF16, DTYPE_F16 = 0, 1, 2

