@@ -68,12 +68,21 @@ SYMBOLS = [
                                   C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     ('petmh_logp', C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
     ('petmh_last_error', C.c_char_p, []),
+    # synthetic-TAC generator (include/petsim.h)
+    ('petsim_generate', C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_int, C.c_int] + [C.c_void_p] * 8),
+    ('petsim_last_error', C.c_char_p, []),
     # posterior accuracy metrics (include/petmetrics.h)
     ('petmetrics_moments', C.c_int, [C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p]),
     ('petmetrics_work_doubles', C.c_size_t, [C.c_int]),
     ('petmetrics_last_error', C.c_char_p, []),
 ]
+
+
+class PetsimPrior(C.Structure):
+    _fields_ = [('n_roi', C.c_int), ('n_frames', C.c_int), ('time_vector', C.c_void_p), ('dt', C.c_void_p),
+                ('mu_DVR', C.c_void_p), ('cov_DVR', C.c_void_p), ('mu_R1', C.c_void_p), ('cov_R1', C.c_void_p),
+                ('mu_ref', C.c_void_p), ('cov_ref', C.c_void_p), ('k2p', C.c_double), ('sigma_noise', C.c_void_p)]
 
 
 class PetmhProblem(C.Structure):

@@ -383,8 +383,19 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
   const int total = nM * nN;
   const int bid = blockIdx.x;
   const int xcd = bid & 7, loc = bid >> 3, q8 = total >> 3, r8 = total & 7;
+#ifndef CONV_XCD_MAP
+#define CONV_XCD_MAP 1    // 0: identity, 1: XCD-contiguous slots N-fastest, 2: XCD-contiguous slots M-fastest
+#endif
+#if CONV_XCD_MAP == 0
+  const int slot = bid;
+#else
   const int slot = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+#endif
+#if CONV_XCD_MAP == 2
+  const int n_tile = slot / nM, m_tile = slot - n_tile * nM;
+#else
   const int m_tile = slot / nN, n_tile = slot - m_tile * nN;
+#endif
   const int m0 = m_tile * G::S;
 
   const int NC = a.c1 / G::KC + a.c2 / G::KC;

@@ -144,3 +144,51 @@ def mh_problem(seed=0, prior=None, mean_sigma_noise=0.1):
     return dict(time_vector=truth['time_vector'], tac_ref=truth['tac_ref'], k2p=float(truth['k2p']),
                 y_obs=cond[:N_ROI].astype(np.float64), sigma_noise=truth['sigma_noise'],
                 mu_DVR=prior['mu_DVR'], Cov_DVR=prior['Cov_DVR'], mu_R1=prior['mu_R1'], Cov_R1=prior['Cov_R1'])
+
+
+def dataset_sigma_noise(mean_sigma_noise=0.1, rng=None):
+    """sample_sim_data.py:190-194: per-ROI std drawn once per dataset, scaled per frame."""
+    from scipy.stats import truncnorm
+    rng = np.random.default_rng(0) if rng is None else rng
+    tv, dt = time_grid()
+    sigma_roi = truncnorm.rvs(-1 / 0.3, np.inf, loc=mean_sigma_noise, scale=0.3 * mean_sigma_noise, size=N_ROI,
+                              random_state=rng)
+    lam = np.log(2) / MK_HALF_T
+    return sigma_roi[:, None] / np.sqrt(dt[None, :] * np.exp(-lam * tv[None, :]))
+
+
+def simulate_dataset(n, prior=None, mean_sigma_noise=0.1, seed=0, sample_offset=0, sigma_noise=None, device=None):
+    """GPU synthetic test set (include/petsim.h; sample_sim_data.py:139-215).
+
+    Returns the reference's saved fields (varDVR, varR1, vark2p, vartacref,
+    tac_sampled, tac_noisy_sampled as activity, sigma_noise, time_vector, dt) as
+    CUDA tensors / arrays, plus ``condition`` (n, 49, 54) fp32 = [tac_noisy/dt | tac_ref]
+    (main_script.py:107-113) and the per-sample redraw counts ``attempts``."""
+    import ctypes as C
+
+    import torch
+
+    from . import _lib
+    prior = prior or synthetic_prior()
+    tv, dt = time_grid()
+    if sigma_noise is None:
+        sigma_noise = dataset_sigma_noise(mean_sigma_noise, np.random.default_rng(seed))
+    f = lambda a: np.ascontiguousarray(a, dtype=np.float64)   # noqa: E731
+    keep = [f(tv), f(dt), f(prior['mu_DVR']), f(prior['Cov_DVR']), f(prior['mu_R1']), f(prior['Cov_R1']),
+            f(prior['mu_tac_ref']), f(prior['Cov_tac_ref']), f(sigma_noise)]
+    P = _lib.PetsimPrior(N_ROI, N_FRAMES, *(a.ctypes.data for a in keep[:8]), float(prior['mu_k2p']),
+                         keep[8].ctypes.data)
+    dev = torch.device('cuda', torch.cuda.current_device() if device is None else device)
+    o = lambda *shape: torch.empty(shape, dtype=torch.float64, device=dev)   # noqa: E731
+    DVR, R1, REF, TAC, NOISY = o(n, N_ROI), o(n, N_ROI), o(n, N_FRAMES), o(n, N_ROI, N_FRAMES), o(n, N_ROI, N_FRAMES)
+    cond = torch.empty((n, N_ROI + 1, N_FRAMES), dtype=torch.float32, device=dev)
+    att = torch.empty(n, dtype=torch.int32, device=dev)
+    ptr = lambda t: C.c_void_p(t.data_ptr())   # noqa: E731
+    rc = _lib.lib().petsim_generate(C.byref(P), int(seed), int(sample_offset), int(n), dev.index, ptr(DVR), ptr(R1),
+                                    ptr(REF), ptr(TAC), ptr(NOISY), ptr(cond), ptr(att),
+                                    C.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+    if rc != 0:
+        raise ValueError(_lib.lib().petsim_last_error().decode())
+    return {'varDVR': DVR, 'varR1': R1, 'vark2p': np.full(n, float(prior['mu_k2p'])), 'vartacref': REF,
+            'tac_sampled': TAC, 'tac_noisy_sampled': NOISY, 'sigma_noise': sigma_noise, 'time_vector': tv,
+            'dt': dt, 'condition': cond, 'attempts': att}

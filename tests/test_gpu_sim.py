@@ -1,0 +1,48 @@
+"""GPU synthetic-TAC generator (include/petsim.h) vs its CPU oracle
+(oracle/sim_ref.py, same counter-based stream; SRTM2 pinned to the reference's outputs)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def ds():
+    from pet_posterior_distribution_amd.sim_data import simulate_dataset
+    return simulate_dataset(3, seed=11, sample_offset=5)
+
+
+def test_generator_matches_oracle(ds):
+    from oracle.sim_ref import simulate_sample
+    from pet_posterior_distribution_amd.sim_data import synthetic_prior, time_grid
+    pr = synthetic_prior()
+    tv, dt = time_grid()
+    P = dict(pr, time_vector=tv, dt=dt, k2p=float(pr['mu_k2p']), sigma_noise=ds['sigma_noise'])
+    for b in range(3):
+        ref = simulate_sample(P, 11, 5 + b)
+        np.testing.assert_allclose(ds['varDVR'][b].cpu().numpy(), ref['DVR'], rtol=1e-12)
+        np.testing.assert_allclose(ds['varR1'][b].cpu().numpy(), ref['R1'], rtol=1e-12)
+        np.testing.assert_allclose(ds['vartacref'][b].cpu().numpy(), ref['ref'], rtol=1e-12)
+        np.testing.assert_allclose(ds['tac_sampled'][b].cpu().numpy(), ref['tac'], rtol=1e-9, atol=1e-12)
+        np.testing.assert_allclose(ds['tac_noisy_sampled'][b].cpu().numpy(), ref['noisy'], rtol=1e-9, atol=1e-12)
+    cond = ds['condition'].cpu().numpy()
+    noisy = ds['tac_noisy_sampled'].cpu().numpy()
+    np.testing.assert_allclose(cond[:, :48], noisy / dt[None, None, :], rtol=1e-6)
+    np.testing.assert_allclose(cond[:, 48], ds['vartacref'].cpu().numpy(), rtol=1e-6)
+    assert (ds['attempts'].cpu().numpy() >= 3).all()
+
+
+def test_generator_statistics_and_sharding():
+    from pet_posterior_distribution_amd.sim_data import simulate_dataset, synthetic_prior
+    pr = synthetic_prior()
+    n = 1024
+    d = simulate_dataset(n, seed=3)
+    assert (d['attempts'].cpu().numpy() > 0).all()
+    assert (d['tac_sampled'] >= 0).all() and torch.isfinite(d['tac_noisy_sampled']).all()
+    dvr = d['varDVR'].cpu().numpy()
+    sd = np.sqrt(np.diag(pr['Cov_DVR']))
+    assert np.abs(dvr.mean(0) - pr['mu_DVR']).max() < 5 * sd.max() / np.sqrt(n)
+    # sample g's draw does not depend on how the set is split
+    part = simulate_dataset(16, seed=3, sample_offset=100, sigma_noise=d['sigma_noise'])
+    torch.testing.assert_close(part['tac_noisy_sampled'], d['tac_noisy_sampled'][100:116], rtol=0, atol=0)
