@@ -22,6 +22,10 @@
 #include <type_traits>
 #include <algorithm>
 
+#ifndef CONV_LOADERS
+#define CONV_LOADERS 1
+#endif
+
 // Diagnostic builds only (scripts/micro/conv_micro.hip): bit 1 drops the K-loop DMA,
 // bit 2 the MFMAs, bit 4 the epilogue, bit 8 returns at entry, bit 16 returns after
 // the prologue DMA, bit 32 drops the ring barriers, bit 64 the
@@ -211,6 +215,10 @@ struct ConvGeom {
   static constexpr int SMEM0 = EPI_BYTES > RING ? EPI_BYTES : RING;
   static constexpr int SMEM = SMEM0 > TAIL ? SMEM0 : TAIL;
   static_assert(!PREMAP || EPI_BYTES <= RING, "C tile must not overlap the prefetched maps");
+  // Dedicated loader waves (16-bit 3-stage layers): 4 extra waves issue every LDS-DMA
+  // piece, so the 4 MFMA waves never stall on DMA issue.
+  static constexpr bool LDR = CONV_LOADERS && sizeof(T) == 2 && STAGES == 3;
+  static constexpr int NTH = LDR ? 2 * kThreads : kThreads;
   static_assert(WM * WN == 4, "4 waves");
   static_assert(MT % L == 0, "tile must hold whole samples");
   static_assert(B_BYTES % (16 * kThreads) == 0, "B tile split");
@@ -356,7 +364,7 @@ __device__ __forceinline__ void ring_barrier() {
 }
 
 template <typename T, int KIND>
-__global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
+__global__ __launch_bounds__(2 * kThreads, 1) void conv_kernel(ConvArgs<T> a) {
   using G = ConvGeom<T, KIND>;
   constexpr int L = G::L, TAPS = G::TAPS, PADL = G::PADL, EPI = G::EPI, ROWB = G::ROWB, NT = G::NT;
   constexpr bool UPS = G::UPS;
@@ -370,7 +378,9 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
     if (tid == 1023) a.out[0] = (T)0.f;
     return;
   }
-  const int lane = tid & 63, w = tid >> 6;
+  const int lane = tid & 63, w_all = tid >> 6;
+  const bool loader = G::LDR && w_all >= 4;         // waves 4..7: LDS-DMA issue only
+  const int w = loader ? w_all - 4 : w_all;
   const int wm = w / G::WN, wn = w - wm * G::WN;
   const int h = lane >> 5, lr = lane & 31;
 
@@ -632,6 +642,34 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
   } else {
     // 3-deep ring: chunk kc+2 is in flight while chunk kc is computed; the wait
     // before each barrier retires chunk kc+1 only (counted vmcnt, never 0 mid-loop).
+  if constexpr (G::LDR) {
+    // Loader waves: chunk c lands in stage c % 3; barrier B(c+1) closes the MFMA waves'
+    // work on chunk c, after which stage c % 3 takes chunk c + 3.
+    if (loader) {
+      dma.all(smem, 0, 0, lane);
+      ring_barrier<0>();                                   // B0: chunk 0 landed
+      if (NC > 1) dma.all(smem, 1, 1, lane);
+      if (NC > 2) dma.all(smem, 2, 2, lane);
+      for (int kc = 0; kc < NC; ++kc) {
+        if (kc + 2 < NC) ring_barrier<G::PER>();           // chunk kc+1 landed, kc+2 in flight
+        else ring_barrier<0>();
+        if (kc + 3 < NC) dma.all(smem, kc + 3, kc % 3, lane);
+      }
+    } else {
+      prefetch_maps();
+      ring_barrier<0>();                                   // B0 (maps landed too)
+#if CONV_EXP_MODE & 128
+      st_c0 = __builtin_amdgcn_s_memtime();
+      st_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+      int buf = 0;
+      for (int kc = 0; kc < NC; ++kc) {
+        compute(smem + buf * G::STAGE, No{}, 0, 0);
+        ring_barrier<0>();                                 // B(kc+1): own LDS reads done
+        buf = buf == 2 ? 0 : buf + 1;
+      }
+    }
+  } else {
     // bf16: the prologue lands chunk 0 only; chunk 0's compute issues chunks 1 and 2.
     constexpr bool EARLY = sizeof(T) == 2;
     dma.all(smem, 0, 0, lane);
@@ -681,7 +719,10 @@ __global__ __launch_bounds__(kThreads, 1) void conv_kernel(ConvArgs<T> a) {
       compute(smem + buf * G::STAGE, No{}, 0, 0);
       ring_barrier<0>();
     }
-  }  mfma_bf16(1);   // the last chunk's last step (NS even)
+  }
+  }
+  if (loader) return;   // s_barrier waits only for the waves still running
+  mfma_bf16(1);   // the last chunk's last step (NS even)
 #if CONV_EXP_MODE & 128
   if constexpr (G::STAGES == 3) {   // diagnostic: main-loop cycles and the clock (s_memrealtime = 100 MHz)
     const unsigned long long st_c1 = __builtin_amdgcn_s_memtime(), st_r1 = __builtin_amdgcn_s_memrealtime();
@@ -1103,7 +1144,7 @@ static hipError_t launch_one(const ConvArgs<T>& a, hipStream_t s) {
   if (a.cout % G::NT != 0 || a.c1 % G::KC != 0 || a.c2 % G::KC != 0) return hipErrorInvalidValue;
   const int nM = (a.B + G::S - 1) / G::S;
   const int total = nM * (a.cout / G::NT);
-  hipLaunchKernelGGL((conv_kernel<T, KIND>), dim3(total), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL((conv_kernel<T, KIND>), dim3(total), dim3(G::NTH), 0, s, a);
   return hipGetLastError();
 }
 
