@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstring>
 #include <type_traits>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <string>
@@ -208,6 +209,10 @@ struct petdiff_ctx {
   // workspace
   int B_cap = 0;
   DevBuf s0, p0, s1, p1, s2, p2, d3, u0, b0, u1, b1, u2;
+  DevBuf s0b;                        // second s0 buffer (fused next-step down0 writes it)
+  // run the next step's down0 inside the previous step's up2.block epilogue (generate);
+  // PETDIFF_FUSE_DOWN0=0 restores the standalone down0 launch per step (A/B switch)
+  bool fuse_down0 = true;
   DevBuf xa, xb, tacbuf, tbuf, rng;
   hipStream_t cap_stream = nullptr;
   std::map<std::vector<int>, GraphEntry> graphs;
@@ -274,6 +279,7 @@ int ensure_workspace(petdiff_ctx* h, int B) {
   const size_t e = h->act_bytes();
   const size_t Bz = (size_t)B;
   HIPC(h->s0.alloc(Bz * 48 * 128 * e));
+  HIPC(h->s0b.alloc(Bz * 48 * 128 * e));
   HIPC(h->p0.alloc(Bz * 24 * 128 * e));
   HIPC(h->s1.alloc(Bz * 24 * 256 * e));
   HIPC(h->p1.alloc(Bz * 12 * 256 * e));
@@ -315,6 +321,10 @@ struct StepIO {
   const int* tvec;            // else per-sample t (device)
   const int* tac;             // device or null
   FinalArgs fin;
+  int s0_sel;                 // skip buffer of this step: 0 -> s0, 1 -> s0b
+  bool skip_down0;            // s0/p0 already written by the previous step's fused epilogue
+  bool fuse_next;             // up2.block epilogue also runs down0 of the next step (t = next_t)
+  int next_t;
 };
 
 template <typename T>
@@ -335,6 +345,7 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
     }
     return PETDIFF_OK;
   };
+  void* s0 = io.s0_sel ? h->s0b.p : h->s0.p;
   Down0Args d0{};
   d0.x = io.x_in;
   d0.w0 = h->w0.as<float>();
@@ -343,10 +354,10 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
   d0.tac = io.tac;
   d0.tvec = io.tvec;
   d0.t_uniform = io.t_uniform;
-  d0.s0 = h->s0.p;
+  d0.s0 = s0;
   d0.p0 = h->p0.p;
   d0.B = B;
-  CHK(timed(0, [&] { return launch_down0<T>(d0, s); }));
+  if (!io.skip_down0) CHK(timed(0, [&] { return launch_down0<T>(d0, s); }));
 
   struct LIO { const void* s1; int c1; const void* s2; int c2; void* out; void* pool; };
   const LIO lio[kNumConvLayers] = {
@@ -358,7 +369,7 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
       {h->b0.p, 512, nullptr, 0, h->u1.p, nullptr},
       {h->s1.p, 256, h->u1.p, 256, h->b1.p, nullptr},
       {h->b1.p, 256, nullptr, 0, h->u2.p, nullptr},
-      {h->s0.p, 128, h->u2.p, 128, nullptr, nullptr},
+      {s0, 128, h->u2.p, 128, nullptr, nullptr},
   };
   for (int li = 0; li < kNumConvLayers; ++li) {
     const ConvLayer& cl = kConv[li];
@@ -383,7 +394,20 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
     a.n_tac = h->n_tac;
     a.B = B;
     a.cout = cl.cout;
-    if (li == kNumConvLayers - 1) a.fin = io.fin;
+    if (li == kNumConvLayers - 1) {
+      a.fin = io.fin;
+      a.fin.next = Down0Args{};
+      a.fin.next.t_uniform = -1;
+      if (io.fuse_next) {
+        // p0 is free again (down1 of this step has read it); s0 goes to the other buffer
+        // because this very kernel still reads the current one.
+        a.fin.next = d0;
+        a.fin.next.x = nullptr;
+        a.fin.next.tvec = nullptr;
+        a.fin.next.t_uniform = io.next_t;
+        a.fin.next.s0 = io.s0_sel ? h->s0.p : h->s0b.p;
+      }
+    }
     CHK(timed(1 + li, [&] { return launch_conv<T>(cl.kind, a, s); }));
   }
   return PETDIFF_OK;
@@ -481,6 +505,7 @@ int petdiff_create(const petdiff_config* cfg, const float* weights, size_t n_wei
   h->device = device;
   h->n_out = cfg->learn_variance == PETDIFF_LEARN_FIXED ? cfg->n_par : 2 * cfg->n_par;
   h->spec = make_spec(*cfg, h->n_out);
+  if (const char* e = std::getenv("PETDIFF_FUSE_DOWN0")) h->fuse_down0 = std::atoi(e) != 0;
   const size_t need = h->spec.back().off + h->spec.back().size;
   if (n_weights != need)
     return fail(PETDIFF_ERR_INVALID, "weight blob has " + std::to_string(n_weights) + " values, expected " +
@@ -683,6 +708,12 @@ int petdiff_generate(petdiff_handle h, const float* x_T, const int32_t* tac, con
       io.fin.flag_var_tilde = flag_var_tilde;
       io.fin.x_next = bufs[(i + 1) & 1];
       io.fin.x_all = all_xt ? all_xt + (size_t)i * B * 96 : nullptr;
+      if (h->fuse_down0) {
+        io.s0_sel = i & 1;
+        io.skip_down0 = i > 0;
+        io.fuse_next = i + 1 < n_steps;
+        io.next_t = io.fuse_next ? t_seq[i + 1] : -1;
+      }
       CHK(network(h, io, B, q));
     }
     return PETDIFF_OK;

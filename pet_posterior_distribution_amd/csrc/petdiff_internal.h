@@ -29,6 +29,16 @@ enum Tab : int {
   TAB_C2_OVER_C1, kNTab
 };
 
+struct Down0Args {
+  const float* x;            // [B][48][2]
+  const float* w0;           // [6][2][128], residual folded into tap 2
+  const float* cmap;         // [n_tac][48][128]
+  const float* tmap;         // [T][48][128]
+  const int* tac; const int* tvec; int t_uniform;
+  void* s0; void* p0;        // T*
+  int B;
+};
+
 struct FinalArgs {
   const float* wf;     // [128][n_out] final Conv1D 1x1 kernel
   const float* bf;     // [n_out]
@@ -48,6 +58,10 @@ struct FinalArgs {
   float* var_out;
   float* var_tilde_out;
   float* net_out;      // raw network output [B][n_roi][n_out] or null (then no p_sample)
+  // Fused first layer of the NEXT reverse step (loop mode): when next.t_uniform >= 0 the
+  // epilogue also runs down0 on x_next for its own samples (writing next.s0 / next.p0),
+  // which removes the down0 launch from every step but the first.
+  Down0Args next;
 };
 
 template <typename T>
@@ -68,15 +82,7 @@ struct ConvArgs {
   FinalArgs fin;
 };
 
-struct Down0Args {
-  const float* x;            // [B][48][2]
-  const float* w0;           // [6][2][128], residual folded into tap 2
-  const float* cmap;         // [n_tac][48][128]
-  const float* tmap;         // [T][48][128]
-  const int* tac; const int* tvec; int t_uniform;
-  void* s0; void* p0;        // T*
-  int B;
-};
+
 
 // Launch helpers (unet_kernels.hip).  Return hipError_t.
 template <typename T>

@@ -199,7 +199,9 @@ struct ConvGeom {
   static constexpr int PER = APT + BPT;             // LDS-DMA instructions per wave per chunk
   static constexpr int CT_LD = 2 * NT + 8;          // fp32 C tile, one ROW PAIR [c][2] per line (non-final)
   static constexpr int FIN_LD = 132;                // fp32 C tile row (final epilogue, 16-B aligned)
-  static constexpr int EPI_BYTES = (EPI == EPI_FINAL) ? MT * FIN_LD * 4 + 128 * 4 * 4 + 64 : (MT / 2) * CT_LD * 4;
+  // FINAL: C tile | final kernel [128][4] | x_next rows [MT][2] (fused next-step down0)
+  static constexpr int EPI_BYTES =
+      (EPI == EPI_FINAL) ? MT * FIN_LD * 4 + 128 * 4 * 4 + MT * 2 * 4 + 64 : (MT / 2) * CT_LD * 4;
   static constexpr int RING = STAGES * STAGE;
   // Non-final epilogues: the block's time map [L][NT] and label map [L][NT] (fp32) and
   // the condition index of its samples are prefetched into LDS behind the ring at
@@ -347,6 +349,62 @@ template <> struct Vec8<float> {
     *reinterpret_cast<f32x4*>(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
   }
 };
+
+// down0 positions pos0, pos0 + pstride, ... of samples b0 .. b0 + nb - 1: x from LDS
+// (xs [nb][96]), maps from LDS (mp [48][128], fast) or global, weights in registers.
+template <typename T>
+__device__ __forceinline__ void down0_positions(const Down0Args& a, const float* xs, const float* mp, bool fast,
+                                                int b0, int nb, const f32x4 (&wr)[12][2], int n0, int pos0,
+                                                int pstride) {
+  for (int pos = pos0; pos < nb * 24; pos += pstride) {
+    const int bl = pos / 24, lp = pos - bl * 24, b = b0 + bl;
+    const int l0 = 2 * lp;
+    float xv[7][2];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+      const int p = l0 - 2 + q;
+      const bool ok = (p >= 0 && p < 48);
+      xv[q][0] = ok ? xs[bl * 96 + p * 2] : 0.f;
+      xv[q][1] = ok ? xs[bl * 96 + p * 2 + 1] : 0.f;
+    }
+    float v[2][8];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int l = l0 + e;
+      f32x4 m0, m1;
+      if (fast) {
+        m0 = *reinterpret_cast<const f32x4*>(mp + l * 128 + n0);
+        m1 = *reinterpret_cast<const f32x4*>(mp + l * 128 + n0 + 4);
+      } else {
+        const int tac = a.tac ? a.tac[b] : 0;
+        const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[b];
+        const float* tmr = a.tmap + ((size_t)t * 48 + l) * 128 + n0;
+        const float* cmr = a.cmap + ((size_t)tac * 48 + l) * 128 + n0;
+        m0 = *reinterpret_cast<const f32x4*>(tmr) + *reinterpret_cast<const f32x4*>(cmr);
+        m1 = *reinterpret_cast<const f32x4*>(tmr + 4) + *reinterpret_cast<const f32x4*>(cmr + 4);
+      }
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          acc0 += wr[j * 2 + c][0] * xv[e + j][c];
+          acc1 += wr[j * 2 + c][1] * xv[e + j][c];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[e][q] = fmaxf(acc0[q] + m0[q], 0.f);
+        v[e][4 + q] = fmaxf(acc1[q] + m1[q], 0.f);
+      }
+      Vec8<T>::store(reinterpret_cast<T*>(a.s0) + ((size_t)b * 48 + l) * 128 + n0, v[e]);
+    }
+    float pv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) pv[q] = fmaxf(v[0][q], v[1][q]);
+    Vec8<T>::store(reinterpret_cast<T*>(a.p0) + ((size_t)b * 24 + lp) * 128 + n0, pv);
+  }
+}
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -848,8 +906,10 @@ __global__ __launch_bounds__(2 * kThreads, 1) void conv_kernel(ConvArgs<T> a) {
     // -> p_sample epilogue; one thread per output row.
     float* fin = reinterpret_cast<float*>(smem);
     float* wfl = fin + G::MT * G::FIN_LD;
+    float* xst = wfl + 128 * 4;                       // [MT][2] x_next of this tile's rows
     const FinalArgs& f = a.fin;
     const int n_out = f.n_out;
+    const bool fuse_next = f.next.t_uniform >= 0 && f.x_next != nullptr;
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -918,8 +978,34 @@ __global__ __launch_bounds__(2 * kThreads, 1) void conv_kernel(ConvArgs<T> a) {
           const float xn = mean + (f.flag_var_tilde ? var_t : var);
           f.x_next[idx + c] = xn;
           if (f.x_all) f.x_all[idx + c] = xn;
+          xst[r * 2 + c] = xn;
         }
       }
+    }
+    if (fuse_next) {
+      // down0 of the next reverse step on this tile's samples (x_next from LDS): the
+      // same per-position code as down0_kernel, 16 positions in flight per pass.
+      static_assert(G::MT % L == 0 && L == 48, "fused down0 needs whole 48-ROI samples");
+      static_assert(G::NTH == kThreads, "fused down0 strides assume one 256-thread block");
+      const Down0Args& nd = f.next;
+      const int nb = min(G::MT / L, B - m0);
+      const int tac0 = nd.tac ? nd.tac[m0] : 0;
+      const bool fast = __syncthreads_and(!nd.tac || tid >= nb || nd.tac[m0 + tid] == tac0) != 0;
+      const int n0 = (tid & 15) * 8;
+      f32x4 wr[12][2];
+#pragma unroll
+      for (int jc = 0; jc < 12; ++jc) {
+        wr[jc][0] = *reinterpret_cast<const f32x4*>(nd.w0 + jc * 128 + n0);
+        wr[jc][1] = *reinterpret_cast<const f32x4*>(nd.w0 + jc * 128 + n0 + 4);
+      }
+      float* mp = fin;                                // C tile is dead after the barrier above
+      if (fast) {
+        const f32x4* tm = reinterpret_cast<const f32x4*>(nd.tmap + (size_t)nd.t_uniform * 48 * 128);
+        const f32x4* cm = reinterpret_cast<const f32x4*>(nd.cmap + (size_t)tac0 * 48 * 128);
+        for (int k = tid; k < 48 * 128 / 4; k += kThreads) reinterpret_cast<f32x4*>(mp)[k] = tm[k] + cm[k];
+      }
+      __syncthreads();
+      down0_positions<T>(nd, xst, mp, fast, m0, nb, wr, n0, tid >> 4, kThreads / 16);
     }
   }
 }
@@ -967,54 +1053,7 @@ __global__ __launch_bounds__(512) void down0_kernel(Down0Args a, int spb) {
     for (int k = 0; k < 3; ++k) reinterpret_cast<f32x4*>(mp)[tid + 512 * k] = mv[k];
   }
   __syncthreads();
-  for (int pos = tid >> 4; pos < nb * 24; pos += 32) {
-    const int bl = pos / 24, lp = pos - bl * 24, b = b0 + bl;
-    const int l0 = 2 * lp;
-    float xv[7][2];
-#pragma unroll
-    for (int q = 0; q < 7; ++q) {
-      const int p = l0 - 2 + q;
-      const bool ok = (p >= 0 && p < 48);
-      xv[q][0] = ok ? xs[bl * 96 + p * 2] : 0.f;
-      xv[q][1] = ok ? xs[bl * 96 + p * 2 + 1] : 0.f;
-    }
-    float v[2][8];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int l = l0 + e;
-      f32x4 m0, m1;
-      if (fast) {
-        m0 = *reinterpret_cast<const f32x4*>(mp + l * 128 + n0);
-        m1 = *reinterpret_cast<const f32x4*>(mp + l * 128 + n0 + 4);
-      } else {
-        const int tac = a.tac ? a.tac[b] : 0;
-        const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[b];
-        const float* tmr = a.tmap + ((size_t)t * 48 + l) * 128 + n0;
-        const float* cmr = a.cmap + ((size_t)tac * 48 + l) * 128 + n0;
-        m0 = *reinterpret_cast<const f32x4*>(tmr) + *reinterpret_cast<const f32x4*>(cmr);
-        m1 = *reinterpret_cast<const f32x4*>(tmr + 4) + *reinterpret_cast<const f32x4*>(cmr + 4);
-      }
-      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          acc0 += wr[j * 2 + c][0] * xv[e + j][c];
-          acc1 += wr[j * 2 + c][1] * xv[e + j][c];
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        v[e][q] = fmaxf(acc0[q] + m0[q], 0.f);
-        v[e][4 + q] = fmaxf(acc1[q] + m1[q], 0.f);
-      }
-      Vec8<T>::store(reinterpret_cast<T*>(a.s0) + ((size_t)b * 48 + l) * 128 + n0, v[e]);
-    }
-    float pv[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) pv[q] = fmaxf(v[0][q], v[1][q]);
-    Vec8<T>::store(reinterpret_cast<T*>(a.p0) + ((size_t)b * 24 + lp) * 128 + n0, pv);
-  }
+  down0_positions<T>(a, xs, mp, fast, b0, nb, wr, n0, tid >> 4, 32);
 }
 
 // ---------------------------------------------------------------------------

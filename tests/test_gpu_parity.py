@@ -272,3 +272,30 @@ def test_loop_tac_major_graph_bf16(m16, conds):
     a = m16.ddpm_loop(x[:B // 2], conds[:1], num_timesteps=30, seed=9, sample_offset=0)
     b = m16.ddpm_loop(x[B // 2:], conds[1:], num_timesteps=30, seed=9, sample_offset=B // 2)
     torch.testing.assert_close(both, torch.cat([a, b]), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize('dtype', ['bfloat16', 'float32'])
+def test_fused_next_step_down0_bitwise(conds, dtype, monkeypatch):
+    """The loop runs step i+1's first layer (down0) inside step i's final-conv epilogue;
+    PETDIFF_FUSE_DOWN0=0 keeps the standalone down0 launch.  Same arithmetic either way:
+    bit-identical samples, for a ragged batch with conditions interleaved per sample
+    (the epilogue's per-row map path) and for a single condition (the LDS map path)."""
+    rng = np.random.default_rng(23)
+    B = 37
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    table = np.stack([conds[0], conds[1], conds[0] * 0.9 + 0.05])
+    tac = rng.integers(0, 3, B).astype(np.int32)
+    monkeypatch.setenv('PETDIFF_FUSE_DOWN0', '0')
+    plain = make_model(dtype)
+    plain._ensure_handle()                    # the switch is read when the handle is created
+    monkeypatch.setenv('PETDIFF_FUSE_DOWN0', '1')
+    fused = make_model(dtype)
+    fused._ensure_handle()
+    for kw in ({'tac': tac}, {}):
+        cset = table if kw else conds[:1]
+        for g in (True, False):
+            a = plain.ddpm_loop(x, cset, num_timesteps=25, seed=4, use_graph=g, **kw)
+            b = fused.ddpm_loop(x, cset, num_timesteps=25, seed=4, use_graph=g, **kw)
+            torch.testing.assert_close(a, b, rtol=0, atol=0)
+    plain.close()
+    fused.close()
