@@ -924,6 +924,33 @@ __global__ __launch_bounds__(2 * kThreads, 1) void conv_kernel(ConvArgs<T> a) {
       const int nn = e >> 2, o = e & 3;
       wfl[e] = o < n_out ? f.wf[nn * n_out + o] : 0.f;
     }
+    // Fused next-step down0: its weights and (single-condition) map rows are loaded into
+    // registers here so their latency hides behind the row loop below.
+    static_assert(G::MT % L == 0 && L == 48, "fused down0 needs whole 48-ROI samples");
+    static_assert(G::NTH == kThreads, "fused down0 strides assume one 256-thread block");
+    const Down0Args& nd = f.next;
+    const int nb_next = min(G::MT / L, B - m0);
+    const int n0_next = (tid & 15) * 8;
+    int* flag = reinterpret_cast<int*>(xst + G::MT * 2);
+    f32x4 wr[12][2], mv[6];
+    if (fuse_next) {
+      const int tac0 = nd.tac ? nd.tac[m0] : 0;
+      // one condition in the tile?  Wave 0 votes (nb <= 64); no __syncthreads_and, whose
+      // LDS scratch costs the K loop its counted LDS-DMA waits (vmcnt(0) per read group).
+      if (tid < 64) {
+        const unsigned long long ok = __ballot(!nd.tac || tid >= nb_next || nd.tac[m0 + tid] == tac0);
+        if (tid == 0) *flag = ok == ~0ull;
+      }
+#pragma unroll
+      for (int jc = 0; jc < 12; ++jc) {
+        wr[jc][0] = *reinterpret_cast<const f32x4*>(nd.w0 + jc * 128 + n0_next);
+        wr[jc][1] = *reinterpret_cast<const f32x4*>(nd.w0 + jc * 128 + n0_next + 4);
+      }
+      const f32x4* tm = reinterpret_cast<const f32x4*>(nd.tmap + (size_t)nd.t_uniform * 48 * 128);
+      const f32x4* cm = reinterpret_cast<const f32x4*>(nd.cmap + (size_t)tac0 * 48 * 128);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) mv[k] = tm[tid + kThreads * k] + cm[tid + kThreads * k];
+    }
     __syncthreads();
     for (int r = tid; r < G::MT; r += kThreads) {
       const int s = r / L, l = r - s * L, b = m0 + s;
@@ -985,27 +1012,15 @@ __global__ __launch_bounds__(2 * kThreads, 1) void conv_kernel(ConvArgs<T> a) {
     if (fuse_next) {
       // down0 of the next reverse step on this tile's samples (x_next from LDS): the
       // same per-position code as down0_kernel, 16 positions in flight per pass.
-      static_assert(G::MT % L == 0 && L == 48, "fused down0 needs whole 48-ROI samples");
-      static_assert(G::NTH == kThreads, "fused down0 strides assume one 256-thread block");
-      const Down0Args& nd = f.next;
-      const int nb = min(G::MT / L, B - m0);
-      const int tac0 = nd.tac ? nd.tac[m0] : 0;
-      const bool fast = __syncthreads_and(!nd.tac || tid >= nb || nd.tac[m0 + tid] == tac0) != 0;
-      const int n0 = (tid & 15) * 8;
-      f32x4 wr[12][2];
-#pragma unroll
-      for (int jc = 0; jc < 12; ++jc) {
-        wr[jc][0] = *reinterpret_cast<const f32x4*>(nd.w0 + jc * 128 + n0);
-        wr[jc][1] = *reinterpret_cast<const f32x4*>(nd.w0 + jc * 128 + n0 + 4);
-      }
-      float* mp = fin;                                // C tile is dead after the barrier above
+      __syncthreads();                               // x_next rows staged; C tile dead
+      const bool fast = *flag != 0;
+      float* mp = fin;
       if (fast) {
-        const f32x4* tm = reinterpret_cast<const f32x4*>(nd.tmap + (size_t)nd.t_uniform * 48 * 128);
-        const f32x4* cm = reinterpret_cast<const f32x4*>(nd.cmap + (size_t)tac0 * 48 * 128);
-        for (int k = tid; k < 48 * 128 / 4; k += kThreads) reinterpret_cast<f32x4*>(mp)[k] = tm[k] + cm[k];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) reinterpret_cast<f32x4*>(mp)[tid + kThreads * k] = mv[k];
       }
       __syncthreads();
-      down0_positions<T>(nd, xst, mp, fast, m0, nb, wr, n0, tid >> 4, kThreads / 16);
+      down0_positions<T>(nd, xst, mp, fast, m0, nb_next, wr, n0_next, tid >> 4, kThreads / 16);
     }
   }
 }

@@ -1,0 +1,37 @@
+"""Per-layer kernel averages (us) from rocprofv3 kernel_stats CSVs, side by side.
+Usage: python scripts/kstats.py a/run_kernel_stats.csv [b/run_kernel_stats.csv ...]"""
+import csv
+import re
+import sys
+
+LAYERS = ['down1', 'down2', 'down3', 'up0.conv2', 'up0.block', 'up1.conv2', 'up1.block', 'up2.conv2', 'up2.block']
+
+
+def label(name):
+    if 'down0_kernel' in name:
+        return 'down0'
+    m = re.search(r'conv_kernel.*?Li(\d)E', name) or re.search(r'conv_kernel<[^,]*, (\d)>', name)
+    if 'conv_kernel' in name:
+        if m:
+            return LAYERS[int(m.group(1))]
+        return 'down2'          # the demangler garbles the <bf16, 1> instance
+    return None
+
+
+def load(path):
+    out = {}
+    for r in csv.DictReader(open(path)):
+        k = label(r['Name'])
+        if k:
+            out[k] = (int(r['Calls']), float(r['AverageNs']) / 1e3)
+    return out
+
+
+cols = [load(p) for p in sys.argv[1:]]
+keys = ['down0'] + LAYERS
+print('%-10s' % 'kernel' + ''.join('%18s' % ('calls / avg us',) for _ in cols))
+for k in keys:
+    print('%-10s' % k + ''.join('%8s %9.2f' % (c[k][0], c[k][1]) if k in c else '%18s' % '-' for c in cols))
+tot = [sum(n * a for n, a in c.values()) for c in cols]
+steps = [max(n for n, _ in c.values()) for c in cols]
+print('%-10s' % 'us/step' + ''.join('%18.2f' % (t / s) for t, s in zip(tot, steps)))
