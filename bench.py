@@ -32,6 +32,9 @@ UP0_BLOCK_FLOP_PER_SAMPLE = 2 * 12 * 512 * 1024 * 7
 UP0_BLOCK_EXEC_FLOP_PER_SAMPLE = 2 * 12 * 512 * 1024 * 6   # executed (residual folded into the centre tap)
 PEAK_BF16_TFLOPS = 2500.0                   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
+# training step: forward + data grad + weight grad of every layer, incl. the
+# per-sample condition encoder / label projections / time MLP (6,002,304 FLOP per sample forward)
+TRAIN_FLOP_PER_SAMPLE = 3 * (FLOP_PER_SAMPLE_STEP + 6_002_304)
 
 
 def parse():
@@ -46,8 +49,9 @@ def parse():
     ap.add_argument('--dtype', default='bfloat16', choices=['bfloat16', 'float16', 'float32'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-kernel-timing', action='store_true')
-    ap.add_argument('--workload', default='iddpm', choices=['iddpm', 'mh'],
+    ap.add_argument('--workload', default='iddpm', choices=['iddpm', 'mh', 'train'],
                     help='iddpm: BASELINE configs[1] (the metric); mh: configs[2] MH/SRTM2 baseline')
+    ap.add_argument('--train-batch', type=int, default=256, help='training batch per GPU (main_script.py:169)')
     ap.add_argument('--mh-chains', type=int, default=10000)
     ap.add_argument('--mh-iters', type=int, default=10000, help='MH draws per chain (kept)')
     ap.add_argument('--mh-tune', type=int, default=10000, help='MH tuning steps per chain (config 3: 20k steps in total)')
@@ -196,10 +200,123 @@ def main_mh(args):
         dist.destroy_process_group()
 
 
+def train_cpu_baseline(weights, x0, cond, budget_s=12.0):
+    """oracle/train_ref.py (NumPy fp64 forward + backward) on a bounded sample."""
+    from oracle import iddpm_ref as R
+    from oracle import train_ref as TR
+    S = R.schedule_tables(R.get_beta_schedule('cosine', 1000))
+    P = {k: v.astype(np.float64) for k, v in weights.items()}
+    rng = np.random.default_rng(0)
+    B = 2
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s or n == 0:
+        TR.train_loss_and_grads(P, S, x0[:B], cond[:B], rng.integers(0, 1000, B), rng.standard_normal((B, 48, 2)))
+        n += 1
+    dt = time.perf_counter() - t0
+    return {'value': n * B / dt, 'unit': 'training samples/s', 'cores': host_threads(), 'kind': 'port',
+            'sample': f'oracle/train_ref.py (NumPy fp64, loss + full backward, no optimizer), {n} batches of {B} '
+                      f'({dt:.1f} s)'}
+
+
+def main_train(args):
+    """ImprovedDDPM.train_step at the reference's batch (256 per GPU), fp32.
+    Data-parallel over ranks: per-rank gradients summed over RCCL and averaged
+    (apply_gradients(1/world)); training data = the GPU synthetic-TAC generator (row 3)."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        os.environ.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device('cuda', torch.cuda.current_device())
+    from pet_posterior_distribution_amd import ImprovedDDPM, UnetConditional, Adam, ExponentialDecay
+    from pet_posterior_distribution_amd.configs import shipped_net_args, shipped_diff_args
+    from pet_posterior_distribution_amd.networks import glorot_uniform_init
+    from pet_posterior_distribution_amd.sim_data import simulate_dataset
+    net = UnetConditional(**shipped_net_args(), seed=1234)
+    net.build((None, 48, 2))
+    net.weights = glorot_uniform_init(net.spec(), seed=1234)
+    model = ImprovedDDPM(network=net, dtype='float32', device=dev.index, **shipped_diff_args())
+    B = args.train_batch
+    n_data = B * 8
+    # main_script.py:169-192, 233: Adam(ExponentialDecay(2e-4 -> 5e-5 over 500 epochs), clipnorm 1.5)
+    sched = ExponentialDecay(2e-4, n_data // B, (5e-5 / 2e-4) ** (1 / 500))
+    model.compile(optimizer=Adam(learning_rate=sched, clipnorm=1.5), loss='MeanSquaredError')
+    data = simulate_dataset(n_data, seed=7, sample_offset=rank * n_data, device=dev.index)
+    x0 = torch.stack([data['varDVR'], data['varR1']], -1).to(torch.float32).contiguous()
+    cond = data['condition']
+    tr = model._ensure_trainer()
+    loss = torch.empty(B, dtype=torch.float32, device=dev)
+    it = [0]
+
+    def one():
+        k = it[0] % 8
+        it[0] += 1
+        tr.compute_gradients(x0[k * B:(k + 1) * B], cond[k * B:(k + 1) * B], seed=11,
+                             sample_offset=rank * B, loss=loss)
+        if world > 1:
+            g = tr.gradients()
+            dist.all_reduce(g)
+            tr.set_gradients(g)
+        tr.apply_gradients(1.0 / world)
+
+    for _ in range(max(args.warmup, 1)):
+        one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    stats = tr.last_stats()
+    if rank == 0:
+        samples = world * B * args.steps
+        value = samples / elapsed
+        ach = TRAIN_FLOP_PER_SAMPLE * samples / elapsed / 1e12
+        line = {
+            'metric': 'training samples/sec (ImprovedDDPM.train_step, batch 256 per GPU)', 'value': round(value, 1),
+            'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': None, 'dtype': 'f32',
+            'data': 'synthetic (GPU SRTM2 generator: truncated-MVN priors + noise model; Glorot init)',
+            'config': {'workload': 'iDDPM training step (q-sample, U-Net fwd/bwd, MSE + 0.1 VLB, clipped Adam)',
+                       'batch_per_gpu': B, 'global_batch': world * B,
+                       'parallelism': f'dp{world} (RCCL all-reduce of the fp32 gradient blob)'},
+            'roofline': {'bound': 'mfma', 'scope': 'whole step (rocBLAS fp32 GEMMs + HIP glue)',
+                         'achieved': round(ach, 2), 'peak': PEAK_F32_TFLOPS, 'unit': 'TFLOP/s',
+                         'frac': round(ach / PEAK_F32_TFLOPS, 4), 'traffic': None,
+                         'flop_per_sample': TRAIN_FLOP_PER_SAMPLE},
+            'last_loss': [round(float(v), 6) for v in stats],
+        }
+        line['cpu_baseline'] = None if (world > 1 or args.no_cpu_baseline) else \
+            train_cpu_baseline(net.weights, x0[:2].cpu().numpy(), cond[:2].cpu().numpy())
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if args.workload == 'mh':
         return main_mh(args)
+    if args.workload == 'train':
+        return main_train(args)
     import torch
     import torch.distributed as dist
     world = int(os.environ.get('WORLD_SIZE', '1'))

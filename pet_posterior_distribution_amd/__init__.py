@@ -8,6 +8,7 @@ from . import _lib
 from .helper_func import get_beta_schedule, cos_beta_schedule, chunker
 from .networks import UnetConditional, param_spec, glorot_uniform_init, denoiser_init
 from .diffusion_model import ImprovedDDPM, summarize_stats
+from .training import Adam, ExponentialDecay
 
 __all__ = ['ImprovedDDPM', 'UnetConditional', 'get_beta_schedule', 'cos_beta_schedule', 'chunker',
-           'param_spec', 'glorot_uniform_init', 'denoiser_init', 'summarize_stats']
+           'param_spec', 'glorot_uniform_init', 'denoiser_init', 'summarize_stats', 'Adam', 'ExponentialDecay']

@@ -79,6 +79,33 @@ SYMBOLS = [
 ]
 
 
+class PettrainConfig(C.Structure):
+    _fields_ = [('learning_rate', C.c_float), ('decay_steps', C.c_float), ('decay_rate', C.c_float),
+                ('beta_1', C.c_float), ('beta_2', C.c_float), ('epsilon', C.c_float), ('clipnorm', C.c_float),
+                ('lambda_vlb', C.c_float)]
+
+
+SYMBOLS += [
+    # training step (include/pettrain.h)
+    ('pettrain_default_config', C.c_int, [C.POINTER(PettrainConfig)]),
+    ('pettrain_create', C.c_int, [C.POINTER(PetdiffConfig), C.c_void_p, C.c_size_t, C.c_void_p, C.c_int,
+                                  C.POINTER(PettrainConfig), C.c_int, C.POINTER(C.c_void_p)]),
+    ('pettrain_destroy', None, [C.c_void_p]),
+    ('pettrain_compute_gradients', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                             C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]),
+    ('pettrain_apply_gradients', C.c_int, [C.c_void_p, C.c_float, C.c_void_p]),
+    ('pettrain_step', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64,
+                                C.c_uint64, C.c_void_p, C.c_void_p]),
+    ('pettrain_gradients', C.c_void_p, [C.c_void_p]),
+    ('pettrain_get_weights', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    ('pettrain_get_gradients', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    ('pettrain_set_gradients', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    ('pettrain_last_stats', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    ('pettrain_iterations', C.c_int64, [C.c_void_p]),
+    ('pettrain_last_error', C.c_char_p, []),
+]
+
+
 class PetsimPrior(C.Structure):
     _fields_ = [('n_roi', C.c_int), ('n_frames', C.c_int), ('time_vector', C.c_void_p), ('dt', C.c_void_p),
                 ('mu_DVR', C.c_void_p), ('cov_DVR', C.c_void_p), ('mu_R1', C.c_void_p), ('cov_R1', C.c_void_p),

@@ -126,6 +126,9 @@ class ImprovedDDPM:
         self._call_counter = 0
         self._handle = None
         self._cond_cache = None     # (unique-conditions tensor) last sent to the library
+        self._trainer = None
+        self._weights_stale = False
+        self.optimizer = None
         self.name = 'improved_ddpm'
 
     # ------------------------------------------------------------------ setup
@@ -139,12 +142,9 @@ class ImprovedDDPM:
                 1.0 / c1, c2 / c1]
         return np.ascontiguousarray(np.stack([np.asarray(r, dtype=NP_DTYPE) for r in rows]))
 
-    def _ensure_handle(self):
-        if self._handle is not None:
-            return self._handle
+    def _c_config(self):
+        """petdiff_config of this model (shipped architecture, schedule length, variance / target)."""
         L = _lib.lib()
-        if self.network.weights is None:
-            self.network.build((None, 48, 2))
         cfg = _lib.PetdiffConfig()
         _lib.check(L.petdiff_default_config(C.byref(cfg)))
         cfg.timesteps = self.timesteps
@@ -156,6 +156,16 @@ class ImprovedDDPM:
                                 _lib.PARAM_X0 if p in self.x0_param_name_list else
                                 _lib.PARAM_V if p in self.v_param_name_list else _lib.PARAM_EPS)
         cfg.dtype = self.dtype
+        return cfg
+
+    def _ensure_handle(self):
+        if self._handle is not None:
+            return self._handle
+        L = _lib.lib()
+        self._sync_trained_weights()
+        if self.network.weights is None:
+            self.network.build((None, 48, 2))
+        cfg = self._c_config()
         blob = self.network.flat_weights()
         h = C.c_void_p()
         torch.cuda.set_device(self.device)
@@ -166,6 +176,119 @@ class ImprovedDDPM:
         _lib.check(L.petdiff_set_schedule(h, tabs.ctypes.data_as(C.c_void_p), self.timesteps),
                    'petdiff_set_schedule')
         return h
+
+    # ------------------------------------------------------------------ training (8(f) row 4)
+    def compile(self, optimizer=None, loss='MeanSquaredError', **kwargs):
+        """keras Model.compile as used by the reference (main_script.py:233-234)."""
+        from .training import Adam, _Mean
+        self._sync_trained_weights()
+        name = loss if isinstance(loss, str) else getattr(loss, '__name__', type(loss).__name__)
+        if str(name).replace('_', '').lower() not in ('meansquarederror', 'mse'):
+            raise NotImplementedError('only the MeanSquaredError loss of the reference is supported')
+        self.optimizer = optimizer if optimizer is not None else Adam()
+        self.loss_tracker = _Mean('loss')
+        self.noise_loss_tracker = _Mean('noise_loss')
+        self.lambda_vlb_loss_tracker = _Mean('lambda_vlb_loss')
+        self._trainer = None
+        self._train_seed = self.seed
+
+    @property
+    def metrics(self):
+        return [self.loss_tracker, self.noise_loss_tracker, self.lambda_vlb_loss_tracker]
+
+    def _ensure_trainer(self):
+        from .training import Trainer
+        if getattr(self, 'optimizer', None) is None:
+            raise RuntimeError('call compile(optimizer=...) before training')
+        if self._trainer is None:
+            self._sync_trained_weights()
+            self._trainer = Trainer(self, self.optimizer)
+        return self._trainer
+
+    def _sync_trained_weights(self):
+        """Pull the trainer's weights into network.weights (inference handles re-pack them)."""
+        tr = getattr(self, '_trainer', None)
+        if tr is None or not getattr(self, '_weights_stale', False):
+            return
+        blob = tr.weights().cpu().numpy()
+        new, o = {}, 0
+        for n, sh in self.network.spec():
+            k = int(np.prod(sh))
+            new[n] = blob[o:o + k].reshape(sh).copy()
+            o += k
+        self.network.weights = new
+        self._weights_stale = False
+
+    def _train_batch(self, data, t, noise, update):
+        images, condition = (data[0], data[1]) if isinstance(data, (tuple, list)) else (data, None)
+        if condition is None:
+            raise NotImplementedError('the shipped UnetConditional requires a condition')
+        tr = self._ensure_trainer()
+        x0 = _as_device(images, self.device, torch.float32)
+        B = x0.shape[0]
+        if tuple(x0.shape[1:]) != (48, 2):
+            raise ValueError(f'images must be (B, 48, 2), got {tuple(x0.shape)}')
+        cond = _as_device(condition, self.device, torch.float32)
+        if tuple(cond.shape) != (B, 49, 54):
+            raise ValueError(f'condition must be (B, 49, 54), got {tuple(cond.shape)}')
+        tt = None if t is None else self._time(t, B)
+        nz = None if noise is None else _as_device(noise, self.device, torch.float32)
+        if nz is not None and nz.shape != x0.shape:
+            raise ValueError('noise must have the shape of images')
+        loss = torch.empty(B, dtype=torch.float32, device=self.device)
+        tr.compute_gradients(x0, cond, tt, nz, seed=self._train_seed, loss=loss)
+        if update:
+            tr.apply_gradients(1.0)
+            self._weights_stale = True
+            self.close()
+        mean_loss, noise_loss, mean_vlb = tr.last_stats()
+        self.loss_tracker.update_state(mean_loss * B, B)
+        self.noise_loss_tracker.update_state(noise_loss, 1)
+        self.lambda_vlb_loss_tracker.update_state(mean_vlb * B, B)
+        self.last_loss = loss
+        return {m.name: m.result() for m in self.metrics}
+
+    def train_step(self, data, t=None, noise=None):
+        """ImprovedDDPM.train_step (diffusion_model.py:533-598): one Adam step on (images, condition).
+        ``t`` / ``noise`` inject the draws (else counter-based Philox)."""
+        return self._train_batch(data, t, noise, update=True)
+
+    def test_step(self, data, t=None, noise=None):
+        """ImprovedDDPM.test_step (diffusion_model.py:600-640): loss only."""
+        return self._train_batch(data, t, noise, update=False)
+
+    def fit(self, x=None, y=None, batch_size=32, epochs=1, validation_split=0.0, shuffle=True, verbose=0,
+            callbacks=None, **kwargs):
+        """keras Model.fit as the reference calls it (main_script.py:267-271): per epoch, shuffled
+        batches through train_step, then test_step over the held-out validation tail."""
+        x = np.asarray(x, dtype=np.float32) if not isinstance(x, torch.Tensor) else x
+        y = np.asarray(y, dtype=np.float32) if not isinstance(y, torch.Tensor) else y
+        n = x.shape[0]
+        n_val = int(n * validation_split)
+        n_tr = n - n_val
+        xd = _as_device(x, self.device, torch.float32)
+        yd = _as_device(y, self.device, torch.float32)
+        rng = np.random.default_rng(self.seed)
+        history = {m.name: [] for m in self.metrics}
+        if n_val:
+            history.update({'val_' + m.name: [] for m in self.metrics})
+        for _ in range(epochs):
+            for m in self.metrics:
+                m.reset_state()
+            order = rng.permutation(n_tr) if shuffle else np.arange(n_tr)
+            for s in range(0, n_tr, batch_size):
+                idx = torch.as_tensor(order[s:s + batch_size], device=self.device)
+                self.train_step((xd[idx], yd[idx]))
+            for m in self.metrics:
+                history[m.name].append(m.result())
+            if n_val:
+                for m in self.metrics:
+                    m.reset_state()
+                for s in range(n_tr, n, batch_size):
+                    self.test_step((xd[s:min(s + batch_size, n)], yd[s:min(s + batch_size, n)]))
+                for m in self.metrics:
+                    history['val_' + m.name].append(m.result())
+        return history
 
     def load_weights(self, path):
         self.network.load_weights(path)
