@@ -43,34 +43,32 @@ __global__ void im2col_kernel(ConvIn ci, int B, const float* lab, const float* t
                               const float* x2, float* A) {
   // rows of K + 1: the last column is 1, so the GEMMs against [W ; bias] add the bias in the
   // forward pass and produce the bias gradient as the last row of the weight gradient.
+  // One block per output row m = (b, l); threads walk the row's taps x channels.
   const int Cf = ci.cfull(), Lout = ci.lout();
   const int Kd = ci.taps * Cf, ld = Kd + 1;
-  const size_t n = (size_t)B * Lout * ld;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const size_t m = i / ld;
-    const int k = (int)(i - m * ld);
-    float v = 1.0f;
-    if (k < Kd) {
-      const int j = k / Cf, c = k - j * Cf;
-      const int l = (int)(m % Lout), b = (int)(m / Lout);
-      const int p = l + j - ci.padl;
-      v = (p >= 0 && p < Lout) ? conv_src(ci, b, ci.ups ? p >> 1 : p, c, lab, tim, x1, x2) : 0.f;
-    }
-    A[i] = v;
+  const int m = blockIdx.x;
+  const int l = m % Lout, b = m / Lout;
+  float* row = A + (size_t)m * ld;
+  for (int j = 0; j < ci.taps; ++j) {
+    const int p = l + j - ci.padl;
+    const bool in = p >= 0 && p < Lout;
+    const int sp = ci.ups ? p >> 1 : p;
+    for (int c = threadIdx.x; c < Cf; c += blockDim.x)
+      row[j * Cf + c] = in ? conv_src(ci, b, sp, c, lab, tim, x1, x2) : 0.f;
   }
+  if (threadIdx.x == 0) row[Kd] = 1.0f;
 }
 
 // dX(b, sp, c) = sum over the fine positions p of sp and the taps j of dA[(b, p - j + padl), j, c]
+// one block per source row (b, sp); threads walk the channels
 __global__ void col2im_kernel(ConvIn ci, int B, const float* dA, float* dlab, float* dtim, float* dx1,
                               float* dx2) {
   const int Cf = ci.cfull(), Lout = ci.lout();
-  const size_t n = (size_t)B * ci.Lsrc * Cf;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const int c = (int)(i % Cf);
-    const size_t r = i / Cf;
-    const int sp = (int)(r % ci.Lsrc), b = (int)(r / ci.Lsrc);
+  const int r = blockIdx.x;
+  const int sp = r % ci.Lsrc, b = r / ci.Lsrc;
+  const int np = ci.ups ? 2 : 1;
+  for (int c = threadIdx.x; c < Cf; c += blockDim.x) {
     float acc = 0.f;
-    const int np = ci.ups ? 2 : 1;
     for (int q = 0; q < np; ++q) {
       const int p = ci.ups ? 2 * sp + q : sp;
       for (int j = 0; j < ci.taps; ++j) {
@@ -405,10 +403,17 @@ __global__ void loss_finish_kernel(const float* sse, const float* vlb, const flo
   const double mse = s_sse[0] / (double)n_el;
   if (loss_out)
     for (int b = threadIdx.x; b < B; b += blockDim.x) loss_out[b] = (float)mse + vlb[b];
-  if (threadIdx.x < n_out) {
-    float g = 0.f;
-    for (int b = 0; b < B; ++b) g += dbias_part[(size_t)b * n_out + threadIdx.x];
-    dbias[threadIdx.x] = g;
+  for (int q = 0; q < n_out; ++q) {           // fixed-order tree over samples
+    __syncthreads();
+    double g = 0.0;
+    for (int b = threadIdx.x; b < B; b += blockDim.x) g += dbias_part[(size_t)b * n_out + q];
+    s_sse[threadIdx.x] = g;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+      if (threadIdx.x < o) s_sse[threadIdx.x] += s_sse[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) dbias[q] = (float)s_sse[0];
   }
   if (threadIdx.x == 0) {
     stats[0] = mse + s_vlb[0] / B;
@@ -481,15 +486,13 @@ __global__ void adam_kernel(AdamArgs a) {
 
 hipError_t im2col(const ConvIn& ci, int B, const float* lab, const float* tim, const float* x1, const float* x2,
                   float* A, hipStream_t s) {
-  const size_t n = (size_t)B * ci.lout() * ci.taps * ci.cfull();
-  hipLaunchKernelGGL(im2col_kernel, dim3(blocks_for(n)), dim3(kT), 0, s, ci, B, lab, tim, x1, x2, A);
+  hipLaunchKernelGGL(im2col_kernel, dim3(B * ci.lout()), dim3(kT), 0, s, ci, B, lab, tim, x1, x2, A);
   return hipGetLastError();
 }
 
 hipError_t col2im(const ConvIn& ci, int B, const float* dA, float* dlab, float* dtim, float* dx1, float* dx2,
                   hipStream_t s) {
-  const size_t n = (size_t)B * ci.Lsrc * ci.cfull();
-  hipLaunchKernelGGL(col2im_kernel, dim3(blocks_for(n)), dim3(kT), 0, s, ci, B, dA, dlab, dtim, dx1, dx2);
+  hipLaunchKernelGGL(col2im_kernel, dim3(B * ci.Lsrc), dim3(kT), 0, s, ci, B, dA, dlab, dtim, dx1, dx2);
   return hipGetLastError();
 }
 
