@@ -220,8 +220,9 @@ def train_cpu_baseline(weights, x0, cond, budget_s=12.0):
 
 def main_train(args):
     """ImprovedDDPM.train_step at the reference's batch (256 per GPU), fp32.
-    Data-parallel over ranks: per-rank gradients summed over RCCL and averaged
-    (apply_gradients(1/world)); training data = the GPU synthetic-TAC generator (row 3)."""
+    Data-parallel over ranks: the per-rank gradients are summed over RCCL, which is exactly the
+    gradient of the global batch on one device (J = B*mse + sum vlb splits over shards;
+    tests/test_cpu_train.py gloo test); training data = the GPU synthetic-TAC generator (row 3)."""
     import torch
     import torch.distributed as dist
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -263,7 +264,7 @@ def main_train(args):
             g = tr.gradients()
             dist.all_reduce(g)
             tr.set_gradients(g)
-        tr.apply_gradients(1.0 / world)
+        tr.apply_gradients(1.0)
 
     for _ in range(max(args.warmup, 1)):
         one()

@@ -114,6 +114,8 @@ struct DevBuf {
   template <typename T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+constexpr int kMaxSplit = 2;   // sample ranges of a split generate (PETDIFF_SPLIT)
+
 struct GraphEntry {
   hipGraphExec_t exec = nullptr;
   hipGraph_t graph = nullptr;
@@ -147,6 +149,9 @@ struct petdiff_ctx {
   bool fuse_down0 = true;
   DevBuf xa, xb, tacbuf, tbuf, rng;
   hipStream_t cap_stream = nullptr;
+  hipStream_t split_stream = nullptr;  // second launch stream of a split generate (PETDIFF_SPLIT)
+  hipEvent_t split_ev[2] = {nullptr, nullptr};
+  int split = 1;
   std::map<std::vector<int>, GraphEntry> graphs;
   // timing
   bool timing = false;
@@ -227,7 +232,7 @@ int ensure_workspace(petdiff_ctx* h, int B) {
   HIPC(h->xb.alloc(Bz * 96 * 4));
   HIPC(h->tacbuf.alloc(Bz * 4));
   HIPC(h->tbuf.alloc(Bz * 4));
-  HIPC(h->rng.alloc(16));
+  HIPC(h->rng.alloc(16 * kMaxSplit));
   // workspace moved: cached graphs hold stale pointers
   for (auto& kv : h->graphs) {
     if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
@@ -257,6 +262,7 @@ struct StepIO {
   bool skip_down0;            // s0/p0 already written by the previous step's fused epilogue
   bool fuse_next;             // up2.block epilogue also runs down0 of the next step (t = next_t)
   int next_t;
+  int b_off;                  // first sample of this launch inside the workspace (split streams)
 };
 
 template <typename T>
@@ -277,7 +283,24 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
     }
     return PETDIFF_OK;
   };
-  void* s0 = io.s0_sel ? h->s0b.p : h->s0.p;
+  // workspace buffers are sample-major: a launch over samples [b_off, b_off + B) uses slices
+  const size_t e = h->act_bytes(), bo = (size_t)io.b_off;
+  auto ws = [&](const DevBuf& d, size_t per_sample) -> void* {
+    return static_cast<char*>(d.p) + bo * per_sample * e;
+  };
+  void* s0 = io.s0_sel ? ws(h->s0b, 48 * 128) : ws(h->s0, 48 * 128);
+  void* s0_other = io.s0_sel ? ws(h->s0, 48 * 128) : ws(h->s0b, 48 * 128);
+  void* p0 = ws(h->p0, 24 * 128);
+  void* s1 = ws(h->s1, 24 * 256);
+  void* p1 = ws(h->p1, 12 * 256);
+  void* s2 = ws(h->s2, 12 * 512);
+  void* p2 = ws(h->p2, 6 * 512);
+  void* d3 = ws(h->d3, 6 * 1024);
+  void* u0 = ws(h->u0, 12 * 512);
+  void* b0 = ws(h->b0, 12 * 512);
+  void* u1 = ws(h->u1, 24 * 256);
+  void* b1 = ws(h->b1, 24 * 256);
+  void* u2 = ws(h->u2, 48 * 128);
   Down0Args d0{};
   d0.x = io.x_in;
   d0.w0 = h->w0.as<float>();
@@ -287,21 +310,21 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
   d0.tvec = io.tvec;
   d0.t_uniform = io.t_uniform;
   d0.s0 = s0;
-  d0.p0 = h->p0.p;
+  d0.p0 = p0;
   d0.B = B;
   if (!io.skip_down0) CHK(timed(0, [&] { return launch_down0<T>(d0, s); }));
 
   struct LIO { const void* s1; int c1; const void* s2; int c2; void* out; void* pool; };
   const LIO lio[kNumConvLayers] = {
-      {h->p0.p, 128, nullptr, 0, h->s1.p, h->p1.p},
-      {h->p1.p, 256, nullptr, 0, h->s2.p, h->p2.p},
-      {h->p2.p, 512, nullptr, 0, h->d3.p, nullptr},
-      {h->d3.p, 1024, nullptr, 0, h->u0.p, nullptr},
-      {h->s2.p, 512, h->u0.p, 512, h->b0.p, nullptr},
-      {h->b0.p, 512, nullptr, 0, h->u1.p, nullptr},
-      {h->s1.p, 256, h->u1.p, 256, h->b1.p, nullptr},
-      {h->b1.p, 256, nullptr, 0, h->u2.p, nullptr},
-      {s0, 128, h->u2.p, 128, nullptr, nullptr},
+      {p0, 128, nullptr, 0, s1, p1},
+      {p1, 256, nullptr, 0, s2, p2},
+      {p2, 512, nullptr, 0, d3, nullptr},
+      {d3, 1024, nullptr, 0, u0, nullptr},
+      {s2, 512, u0, 512, b0, nullptr},
+      {b0, 512, nullptr, 0, u1, nullptr},
+      {s1, 256, u1, 256, b1, nullptr},
+      {b1, 256, nullptr, 0, u2, nullptr},
+      {s0, 128, u2, 128, nullptr, nullptr},
   };
   for (int li = 0; li < kNumConvLayers; ++li) {
     const ConvLayer& cl = kConv[li];
@@ -337,7 +360,7 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
         a.fin.next.x = nullptr;
         a.fin.next.tvec = nullptr;
         a.fin.next.t_uniform = io.next_t;
-        a.fin.next.s0 = io.s0_sel ? h->s0.p : h->s0b.p;
+        a.fin.next.s0 = s0_other;
       }
     }
     CHK(timed(1 + li, [&] { return launch_conv<T>(cl.kind, a, s); }));
@@ -445,6 +468,12 @@ int petdiff_create(const petdiff_config* cfg, const float* weights, size_t n_wei
   for (auto& s : h->spec) h->off[s.name] = s.off;
   HIPC(hipSetDevice(device));
   HIPC(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
+  if (const char* e = std::getenv("PETDIFF_SPLIT")) h->split = std::max(1, std::min(kMaxSplit, std::atoi(e)));
+  if (h->split > 1) {
+    HIPC(hipStreamCreateWithFlags(&h->split_stream, hipStreamNonBlocking));
+    HIPC(hipEventCreateWithFlags(&h->split_ev[0], hipEventDisableTiming));
+    HIPC(hipEventCreateWithFlags(&h->split_ev[1], hipEventDisableTiming));
+  }
   HIPC(h->w32.alloc(need * 4));
   HIPC(hipMemcpy(h->w32.p, weights, need * 4, hipMemcpyHostToDevice));
   std::vector<float> host(weights, weights + need);
@@ -491,6 +520,9 @@ int petdiff_destroy(petdiff_handle h) {
   }
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
+  if (h->split_stream) (void)hipStreamDestroy(h->split_stream);
+  for (auto& ev : h->split_ev)
+    if (ev) (void)hipEventDestroy(ev);
   delete h;
   return PETDIFF_OK;
 }
@@ -615,10 +647,18 @@ int petdiff_generate(petdiff_handle h, const float* x_T, const int32_t* tac, con
   CHK(ensure_workspace(h, B));
   hipStream_t s = (hipStream_t)stream;
   const size_t xbytes = (size_t)B * h->cfg.n_roi * h->cfg.n_par * 4;
-  static thread_local unsigned long long rp[2];
-  rp[0] = seed;
-  rp[1] = sample_offset;
-  HIPC(hipMemcpyAsync(h->rng.p, rp, 16, hipMemcpyHostToDevice, s));
+  const bool graph = use_graph && !z_all && !all_xt && !h->timing && n_steps > 0;
+  // PETDIFF_SPLIT=2: the batch runs as two independent sample ranges, each its own graph,
+  // on two streams, so one range's launch boundaries overlap the other's main loops.
+  const int parts = (graph && h->split > 1 && B >= 64) ? h->split : 1;
+  int pb[kMaxSplit + 1];
+  for (int k = 0; k <= parts; ++k) pb[k] = k == parts ? B : (int)((long long)B * k / parts / 32 * 32);
+  static thread_local unsigned long long rp[2 * kMaxSplit];
+  for (int k = 0; k < parts; ++k) {
+    rp[2 * k] = seed;
+    rp[2 * k + 1] = sample_offset + (unsigned long long)pb[k];
+  }
+  HIPC(hipMemcpyAsync(h->rng.p, rp, 16 * parts, hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(h->xa.p, x_T, xbytes, hipMemcpyDeviceToDevice, s));
   const int* tacp = nullptr;
   if (tac) {
@@ -626,19 +666,22 @@ int petdiff_generate(petdiff_handle h, const float* x_T, const int32_t* tac, con
     tacp = h->tacbuf.as<int>();
   }
   float* bufs[2] = {h->xa.as<float>(), h->xb.as<float>()};
-  auto enqueue = [&](hipStream_t q) -> int {
+  auto enqueue = [&](hipStream_t q, int k) -> int {
+    const int b0 = pb[k], Bk = pb[k + 1] - pb[k];
     for (int i = 0; i < n_steps; ++i) {
       StepIO io{};
-      io.x_in = bufs[i & 1];
+      io.x_in = bufs[i & 1] + (size_t)b0 * 96;
       io.t_uniform = t_seq[i];
       io.tvec = nullptr;
-      io.tac = tacp;
+      io.tac = tacp ? tacp + b0 : nullptr;
+      io.b_off = b0;
       io.fin = base_final(h);
-      io.fin.x_t = bufs[i & 1];
+      io.fin.rng = h->rng.as<unsigned long long>() + 2 * k;
+      io.fin.x_t = io.x_in;
       io.fin.z = z_all ? z_all + (size_t)i * B * 96 : nullptr;
       io.fin.rng_step = i;
       io.fin.flag_var_tilde = flag_var_tilde;
-      io.fin.x_next = bufs[(i + 1) & 1];
+      io.fin.x_next = bufs[(i + 1) & 1] + (size_t)b0 * 96;
       io.fin.x_all = all_xt ? all_xt + (size_t)i * B * 96 : nullptr;
       if (h->fuse_down0) {
         io.s0_sel = i & 1;
@@ -646,33 +689,45 @@ int petdiff_generate(petdiff_handle h, const float* x_T, const int32_t* tac, con
         io.fuse_next = i + 1 < n_steps;
         io.next_t = io.fuse_next ? t_seq[i + 1] : -1;
       }
-      CHK(network(h, io, B, q));
+      CHK(network(h, io, Bk, q));
     }
     return PETDIFF_OK;
   };
-  const bool graph = use_graph && !z_all && !all_xt && !h->timing && n_steps > 0;
   if (!graph) {
-    CHK(enqueue(s));
+    CHK(enqueue(s, 0));
   } else {
-    std::vector<int> key{B, flag_var_tilde, tac ? 1 : 0, n_steps};
-    key.insert(key.end(), t_seq, t_seq + n_steps);
-    auto it = h->graphs.find(key);
-    if (it == h->graphs.end()) {
-      GraphEntry ge;
-      HIPC(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
-      int rc = enqueue(h->cap_stream);
-      hipGraph_t g = nullptr;
-      hipError_t ee = hipStreamEndCapture(h->cap_stream, &g);
-      if (rc != PETDIFF_OK) {
-        if (g) (void)hipGraphDestroy(g);
-        return rc;
+    hipGraphExec_t ex[kMaxSplit];
+    for (int k = 0; k < parts; ++k) {
+      std::vector<int> key{B, flag_var_tilde, tac ? 1 : 0, n_steps, parts, k};
+      key.insert(key.end(), t_seq, t_seq + n_steps);
+      auto it = h->graphs.find(key);
+      if (it == h->graphs.end()) {
+        GraphEntry ge;
+        HIPC(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
+        int rc = enqueue(h->cap_stream, k);
+        hipGraph_t g = nullptr;
+        hipError_t ee = hipStreamEndCapture(h->cap_stream, &g);
+        if (rc != PETDIFF_OK) {
+          if (g) (void)hipGraphDestroy(g);
+          return rc;
+        }
+        HIPC(ee);
+        ge.graph = g;
+        HIPC(hipGraphInstantiate(&ge.exec, g, nullptr, nullptr, 0));
+        it = h->graphs.emplace(key, ge).first;
       }
-      HIPC(ee);
-      ge.graph = g;
-      HIPC(hipGraphInstantiate(&ge.exec, g, nullptr, nullptr, 0));
-      it = h->graphs.emplace(key, ge).first;
+      ex[k] = it->second.exec;
     }
-    HIPC(hipGraphLaunch(it->second.exec, s));
+    if (parts == 1) {
+      HIPC(hipGraphLaunch(ex[0], s));
+    } else {
+      HIPC(hipEventRecord(h->split_ev[0], s));
+      HIPC(hipStreamWaitEvent(h->split_stream, h->split_ev[0], 0));
+      HIPC(hipGraphLaunch(ex[0], s));
+      HIPC(hipGraphLaunch(ex[1], h->split_stream));
+      HIPC(hipEventRecord(h->split_ev[1], h->split_stream));
+      HIPC(hipStreamWaitEvent(s, h->split_ev[1], 0));
+    }
   }
   HIPC(hipMemcpyAsync(x_out, bufs[n_steps & 1], xbytes, hipMemcpyDeviceToDevice, s));
   return PETDIFF_OK;
