@@ -316,11 +316,28 @@ struct DmaPlan {
 
 template <typename T> struct Vec8;
 #ifndef CONV_NT_STORE
-#define CONV_NT_STORE 1   // activation stores with the non-temporal hint (A/B: +3.4% end to end, scripts/ab_bench.sh)
+// activation stores: 1 non-temporal hint (A/B vs plain: +3.4% end to end, scripts/ab_bench.sh);
+// 2 write-through sc1 (A/B vs 1: +2.3%: the next layer reads them on another XCD anyway, and
+// the kernel-end L2 writeback has no dirty lines left to flush); 3 sc0 sc1; 4 sc1 nt
+#define CONV_NT_STORE 2
+#endif
+#if CONV_NT_STORE == 2
+#define CONV_STORE_POLICY "sc1"
+#elif CONV_NT_STORE == 3
+#define CONV_STORE_POLICY "sc0 sc1"
+#elif CONV_NT_STORE == 4
+#define CONV_STORE_POLICY "sc1 nt"
+#else
+#define CONV_STORE_POLICY ""
 #endif
 template <typename V>
 __device__ __forceinline__ void store16(V* p, V v) {
-  if constexpr (CONV_NT_STORE) {
+  if constexpr (CONV_NT_STORE >= 2) {   // inline asm: hipcc counts nothing here, s_nop 1 guards the data VGPRs
+    typedef int i32x4v __attribute__((ext_vector_type(4)));
+    asm volatile("global_store_dwordx4 %0, %1, off " CONV_STORE_POLICY "\n\ts_nop 1" ::"v"(p),
+                 "v"(__builtin_bit_cast(i32x4v, v))
+                 : "memory");
+  } else if constexpr (CONV_NT_STORE) {
     typedef int i32x4v __attribute__((ext_vector_type(4)));
     __builtin_nontemporal_store(__builtin_bit_cast(i32x4v, v), reinterpret_cast<i32x4v*>(p));
   } else {
