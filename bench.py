@@ -30,6 +30,11 @@ FLOP_PER_SAMPLE_STEP = 296_361_984          # x-dependent U-Net convs incl. 1x1 
 # dominant kernel = up0 ConvBlock: relu(conv6(1024->512) + conv1(1024->512)) at L=12 (App. A: 37.75+6.29 M MAC)
 UP0_BLOCK_FLOP_PER_SAMPLE = 2 * 12 * 512 * 1024 * 7
 UP0_BLOCK_EXEC_FLOP_PER_SAMPLE = 2 * 12 * 512 * 1024 * 6   # executed (residual folded into the centre tap)
+# fused up0 level (16-bit default): up0's k2 conv (App. A: 13.20 M MAC, 1074 input channels) + the block
+# in one kernel; executed = skip half (6 taps x 512) + 2-phase composite (4 taps x 1024) + the l = 0, 1
+# left-edge correction rows (1024 -> 512 each)
+UP0_CONV2_FLOP_PER_SAMPLE = 2 * 12 * 2 * 1074 * 512
+UP0_FUSED_EXEC_FLOP_PER_SAMPLE = 2 * 12 * 512 * 512 * 6 + 2 * 12 * 4 * 1024 * 512 + 2 * 2 * 1024 * 512
 PEAK_BF16_TFLOPS = 2500.0                   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
 # training step: forward + data grad + weight grad of every layer, incl. the
@@ -104,13 +109,14 @@ def cpu_baseline(weights, cond, budget_s=15.0):
                       f'extrapolated to 1000 steps'}
 
 
-def load_traffic():
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
+def load_traffic(fused_up=False):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
+    (None when that kernel has no PMC pass on record)."""
     p = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     try:
         with open(p) as f:
             d = json.load(f)
-        return d.get('up0_block_bytes_per_launch')
+        return d.get('up0_fused_bytes_per_launch' if fused_up else 'up0_block_bytes_per_launch')
     except Exception:
         return None
 
@@ -408,11 +414,16 @@ def main():
         if layer_ms is not None:
             ms, cnt = layer_ms['up0.block']
             avg_s = ms / max(cnt, 1) / 1e3
-            ach = UP0_BLOCK_FLOP_PER_SAMPLE * B / avg_s / 1e12
-            roof = {'bound': 'mfma', 'kernel': 'conv_kernel<up0.block> (L=12, 1024->512, k6+res)',
+            fused_up = layer_ms['up0.conv2'][1] == 0      # the k2 conv runs inside the block kernel
+            alg = UP0_BLOCK_FLOP_PER_SAMPLE + (UP0_CONV2_FLOP_PER_SAMPLE if fused_up else 0)
+            exe = UP0_FUSED_EXEC_FLOP_PER_SAMPLE if fused_up else UP0_BLOCK_EXEC_FLOP_PER_SAMPLE
+            ach = alg * B / avg_s / 1e12
+            kname = ('conv_kernel<up0 fused> (UpSampling1D + k2 conv 1074->512 + ConvBlock 1024->512 k6+res, L=12)'
+                     if fused_up else 'conv_kernel<up0.block> (L=12, 1024->512, k6+res)')
+            roof = {'bound': 'mfma', 'kernel': kname,
                     'achieved': round(ach, 2), 'peak': peak, 'unit': 'TFLOP/s', 'frac': round(ach / peak, 4),
-                    'traffic': load_traffic(), 'avg_launch_us': round(avg_s * 1e6, 2),
-                    'executed_tflops': round(UP0_BLOCK_EXEC_FLOP_PER_SAMPLE * B / avg_s / 1e12, 2),
+                    'traffic': load_traffic(fused_up), 'avg_launch_us': round(avg_s * 1e6, 2),
+                    'executed_tflops': round(exe * B / avg_s / 1e12, 2),
                     'pipeline_tflops': round(tflops_pipeline, 2),
                     'pipeline_frac': round(tflops_pipeline / peak, 4)}
         line = {

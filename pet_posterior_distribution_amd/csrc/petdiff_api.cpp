@@ -134,6 +134,10 @@ struct petdiff_ctx {
   DevBuf w0;                         // down0 x weights [6][2][128] fp32 (res folded)
   DevBuf bias_only[kNumConvLayers];  // conv bias + res bias for up blocks
   DevBuf tmap[7], cmap[7];           // per cond level
+  // fused up levels (16-bit path; PETDIFF_FUSE_UP=0 keeps the separate k2-conv launches)
+  bool fuse_up = false;
+  DevBuf wpack_f[3], epack_f[3];     // packed composite weights / left-edge correction weights
+  DevBuf tmap_f[3], cmap_f[3];       // u-path maps through the block conv (+ block biases)
   DevBuf tab;                        // [kNTab][T]
   DevBuf temb, tseq;                 // [T][48], scratch [T][L]
   int T = 0;
@@ -208,6 +212,99 @@ int pack_conv(petdiff_ctx* h, const std::vector<float>& wk_host, int li) {
           }
   HIPC(h->wpack[li].alloc(out.size() * sizeof(H)));
   HIPC(hipMemcpy(h->wpack[li].p, out.data(), out.size() * sizeof(H), hipMemcpyHostToDevice));
+  return PETDIFF_OK;
+}
+
+// Fused up level u (0..2): kinds, the k2 conv and the block it feeds (kConv indices).
+struct FusedLevel {
+  int kind, conv2_li, block_li, cond_level;
+  int L, cs, cb, cout;   // output length, skip channels, coarse-input channels, output channels
+};
+const FusedLevel kFused[3] = {
+    {LK_UP0_F, LK_UP0_CONV2, LK_UP0_BLOCK, 4, 12, 512, 1024, 512},
+    {LK_UP1_F, LK_UP1_CONV2, LK_UP1_BLOCK, 5, 24, 256, 512, 256},
+    {LK_UP2_F, LK_UP2_CONV2, LK_UP2_BLOCK, 6, 48, 128, 256, 128},
+};
+
+// Weights of a fused up level: per N tile, the block's skip-half chunks [6 taps][NT][ROWB]
+// (residual folded into tap 2) then the coarse-input chunks [phase][4 taps][NT][ROWB] of the
+// composite taps (compose_kernel), both with the 16-B pieces XOR-swizzled by n; plus the
+// left-edge correction weights [n_tile][chunk][phase][NT][KC] (plain).
+template <typename T, typename H>
+int pack_fused(petdiff_ctx* h, const std::vector<float>& host, int u) {
+  const FusedLevel& fl = kFused[u];
+  const ConvLayer& blk = kConv[fl.block_li];
+  const ConvLayer& c2 = kConv[fl.conv2_li];
+  const int ROWB = layer_tile(fl.kind).rowb, KC = layer_kc<T>(fl.kind), NT = layer_ntile(fl.kind);
+  const int CPR = ROWB / 16, EPC = 16 / (int)sizeof(T);
+  const int n1 = fl.cs / KC, n2 = fl.cb / KC, nNT = fl.cout / NT;
+  if (fl.cs % KC || fl.cb % KC || fl.cout % NT || n1 < 3 || n2 < 2)
+    return fail(PETDIFF_ERR_UNSUPPORTED, "fused up level geometry");
+  // composite taps on the device (fp64 sums), then packed on the host
+  DevBuf comp;
+  HIPC(comp.alloc((size_t)10 * fl.cb * fl.cout * 4));
+  HIPC(launch_compose(h->W(std::string(c2.wname) + ".kernel"), c2.cin_full, c2.xoff, fl.cb, c2.cout,
+                      h->W(std::string(blk.wname) + ".kernel"), h->W(std::string(blk.resname) + ".kernel"),
+                      blk.cin_full, fl.cs, fl.cout, comp.as<float>(), 0));
+  std::vector<float> D((size_t)10 * fl.cb * fl.cout);
+  HIPC(hipMemcpy(D.data(), comp.p, D.size() * 4, hipMemcpyDeviceToHost));
+  const float* wk = host.data() + h->off.at(std::string(blk.wname) + ".kernel");
+  const float* wr = host.data() + h->off.at(std::string(blk.resname) + ".kernel");
+  auto cvt = [](float v) -> H {
+    if constexpr (std::is_same<T, f16>::value) return f2h(v);
+    else return f2bf(v);
+  };
+  std::vector<H> out((size_t)nNT * (n1 * 6 + n2 * 8) * NT * KC);
+  std::vector<H> eout((size_t)nNT * n2 * 2 * NT * KC);
+  size_t q = 0, qe = 0;
+  for (int nt = 0; nt < nNT; ++nt) {
+    for (int kc = 0; kc < n1; ++kc)
+      for (int j = 0; j < 6; ++j)
+        for (int n = 0; n < NT; ++n)
+          for (int p = 0; p < CPR; ++p) {
+            const int c = p ^ ((n >> 2) & 3);
+            for (int e = 0; e < EPC; ++e) {
+              const int ci = kc * KC + c * EPC + e, co = nt * NT + n;
+              float v = wk[((size_t)j * blk.cin_full + ci) * blk.cout + co];
+              if (j == blk.padl) v += wr[(size_t)ci * blk.cout + co];
+              out[q++] = cvt(v);
+            }
+          }
+    for (int kc = 0; kc < n2; ++kc) {
+      for (int t = 0; t < 8; ++t)
+        for (int n = 0; n < NT; ++n)
+          for (int p = 0; p < CPR; ++p) {
+            const int c = p ^ ((n >> 2) & 3);
+            for (int e = 0; e < EPC; ++e) {
+              const int cb = kc * KC + c * EPC + e, co = nt * NT + n;
+              out[q++] = cvt(D[((size_t)t * fl.cb + cb) * fl.cout + co]);
+            }
+          }
+      for (int ph = 0; ph < 2; ++ph)
+        for (int n = 0; n < NT; ++n)
+          for (int kk = 0; kk < KC; ++kk)
+            eout[qe++] = cvt(D[((size_t)(8 + ph) * fl.cb + kc * KC + kk) * fl.cout + nt * NT + n]);
+    }
+  }
+  HIPC(h->wpack_f[u].alloc(out.size() * sizeof(H)));
+  HIPC(hipMemcpy(h->wpack_f[u].p, out.data(), out.size() * sizeof(H), hipMemcpyHostToDevice));
+  HIPC(h->epack_f[u].alloc(eout.size() * sizeof(H)));
+  HIPC(hipMemcpy(h->epack_f[u].p, eout.data(), eout.size() * sizeof(H), hipMemcpyHostToDevice));
+  return PETDIFF_OK;
+}
+
+// u-path maps of fused level u through its block conv: from the k2 conv's time (+ biases) or
+// label map [n][L][cu] to [n][L][cout] (time: + the block's conv and residual biases)
+int fused_maps(petdiff_ctx* h, int u, bool time, int n, hipStream_t s) {
+  const FusedLevel& fl = kFused[u];
+  const ConvLayer& blk = kConv[fl.block_li];
+  DevBuf& dst = time ? h->tmap_f[u] : h->cmap_f[u];
+  HIPC(dst.alloc((size_t)n * fl.L * fl.cout * 4));
+  const DevBuf& src = time ? h->tmap[fl.cond_level] : h->cmap[fl.cond_level];
+  HIPC(launch_map_through(src.as<float>(), n, fl.L, fl.cout, h->W(std::string(blk.wname) + ".kernel"),
+                          h->W(std::string(blk.resname) + ".kernel"), blk.taps, blk.padl, blk.cin_full, fl.cs,
+                          time ? h->W(std::string(blk.wname) + ".bias") : nullptr,
+                          time ? h->W(std::string(blk.resname) + ".bias") : nullptr, dst.as<float>(), fl.cout, s));
   return PETDIFF_OK;
 }
 
@@ -326,8 +423,46 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
       {b1, 256, nullptr, 0, u2, nullptr},
       {s0, 128, u2, 128, nullptr, nullptr},
   };
+  // fused up levels replace (k2 conv, block) pairs: {kind, timing id, src1, c1, src2, c2, out}
+  const bool fused = sizeof(T) == 2 && h->fuse_up;
   for (int li = 0; li < kNumConvLayers; ++li) {
     const ConvLayer& cl = kConv[li];
+    if (fused && li >= LK_UP0_CONV2) {
+      if (li == LK_UP0_CONV2 || li == LK_UP1_CONV2 || li == LK_UP2_CONV2) continue;
+      const int u = (li - LK_UP0_BLOCK) / 2;
+      const FusedLevel& fl = kFused[u];
+      ConvArgs<T> a{};
+      a.src1 = reinterpret_cast<const T*>(lio[li].s1);                 // the skip
+      a.c1 = fl.cs;
+      a.src2 = reinterpret_cast<const T*>(lio[fl.conv2_li].s1);        // the k2 conv's input
+      a.c2 = fl.cb;
+      a.wpack = h->wpack_f[u].as<T>();
+      a.epack = h->epack_f[u].as<T>();
+      a.out = reinterpret_cast<T*>(lio[li].out);
+      a.tmap = h->tmap_f[u].as<float>();
+      a.cmap = h->cmap_f[u].as<float>();
+      a.tac = io.tac;
+      a.tvec = io.tvec;
+      a.t_uniform = io.t_uniform;
+      a.n_t = h->T;
+      a.n_tac = h->n_tac;
+      a.B = B;
+      a.cout = fl.cout;
+      if (li == kNumConvLayers - 1) {
+        a.fin = io.fin;
+        a.fin.next = Down0Args{};
+        a.fin.next.t_uniform = -1;
+        if (io.fuse_next) {
+          a.fin.next = d0;
+          a.fin.next.x = nullptr;
+          a.fin.next.tvec = nullptr;
+          a.fin.next.t_uniform = io.next_t;
+          a.fin.next.s0 = s0_other;
+        }
+      }
+      CHK(timed(1 + li, [&] { return launch_conv<T>(fl.kind, a, s); }));
+      continue;
+    }
     ConvArgs<T> a{};
     a.src1 = reinterpret_cast<const T*>(lio[li].s1);
     a.c1 = lio[li].c1;
@@ -461,6 +596,8 @@ int petdiff_create(const petdiff_config* cfg, const float* weights, size_t n_wei
   h->n_out = cfg->learn_variance == PETDIFF_LEARN_FIXED ? cfg->n_par : 2 * cfg->n_par;
   h->spec = make_spec(*cfg, h->n_out);
   if (const char* e = std::getenv("PETDIFF_FUSE_DOWN0")) h->fuse_down0 = std::atoi(e) != 0;
+  h->fuse_up = cfg->dtype != PETDIFF_DTYPE_F32;
+  if (const char* e = std::getenv("PETDIFF_FUSE_UP")) h->fuse_up = h->fuse_up && std::atoi(e) != 0;
   const size_t need = h->spec.back().off + h->spec.back().size;
   if (n_weights != need)
     return fail(PETDIFF_ERR_INVALID, "weight blob has " + std::to_string(n_weights) + " values, expected " +
@@ -491,6 +628,11 @@ int petdiff_create(const petdiff_config* cfg, const float* weights, size_t n_wei
       HIPC(hipMemcpy(h->bias_only[li].p, b.data(), cl.cout * 4, hipMemcpyHostToDevice));
     }
   }
+  if (h->fuse_up)
+    for (int u = 0; u < 3; ++u) {
+      if (cfg->dtype == PETDIFF_DTYPE_BF16) CHK((pack_fused<bf16, uint16_t>(h.get(), host, u)));
+      else CHK((pack_fused<f16, uint16_t>(h.get(), host, u)));
+    }
   // down0: x channels 50, 51 of down0.conv (6, 52, 128) with the res kernel folded into tap 2
   {
     std::vector<float> w0(6 * 2 * 128);
@@ -550,6 +692,8 @@ int petdiff_set_schedule(petdiff_handle h, const float* tables, int T) {
                      h->cfg.n_cond_rows, c.res ? h->W(p + ".res.kernel") : nullptr, h->W(cv + ".bias"),
                      c.res ? h->W(p + ".res.bias") : nullptr, h->tmap[lv].as<float>(), c.Lout, c.cout, 0));
   }
+  if (h->fuse_up)
+    for (int u = 0; u < 3; ++u) CHK(fused_maps(h, u, true, T, 0));
   HIPC(hipDeviceSynchronize());
   h->sched_set = true;
   return PETDIFF_OK;
@@ -580,6 +724,8 @@ int petdiff_set_conditions(petdiff_handle h, const float* cond, int n_tac, void*
                      c.cin_full, 0, c.res ? h->W(p + ".res.kernel") : nullptr, nullptr, nullptr,
                      h->cmap[lv].as<float>(), c.Lout, c.cout, s));
   }
+  if (h->fuse_up)
+    for (int u = 0; u < 3; ++u) CHK(fused_maps(h, u, false, n_tac, s));
   if (n_tac != h->n_tac) {
     for (auto& kv : h->graphs) {
       if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);

@@ -68,7 +68,8 @@ template <typename T>
 struct ConvArgs {
   const T* src1; int c1;     // first input (channels-last rows)
   const T* src2; int c2;     // second input (concat [src1 | src2]) or null
-  const T* wpack;            // packed weights [Cout/128][NC][taps][128][4 x 16B]
+  const T* wpack;            // packed weights [Cout/NT][NC][taps][NT][ROWB] (fused: see pack_fused)
+  const T* epack;            // fused up levels: left-edge correction weights [Cout/NT][NC2][2][NT][KC]
   T* out;                    // [B*L][cout]
   T* out_pool;               // [B*L/2][cout] (EPI_POOL)
   const float* cmap;         // [n_tac][L][cout] label contribution or null
@@ -97,6 +98,12 @@ hipError_t launch_dense(const float* in, int rows, int din, const float* w, cons
 hipError_t launch_fold(const float* seq, int n, int Lseq, int Cs, const float* wk, int taps, int padl,
                        int ups, int cin_full, int ch0, const float* wr, const float* b1,
                        const float* b2, float* out, int Lout, int cout, hipStream_t s);
+// fused up levels: composite taps [10][cbn][cout] and u-path maps through the block conv
+hipError_t launch_compose(const float* wup, int cin_up, int xoff, int cbn, int cu, const float* kblk,
+                          const float* kres, int cin_blk, int ch0, int cout, float* out, hipStream_t s);
+hipError_t launch_map_through(const float* in, int n, int L, int cu, const float* kblk, const float* kres, int taps,
+                              int padl, int cin_blk, int ch0, const float* b1, const float* b2, float* out, int cout,
+                              hipStream_t s);
 hipError_t launch_philox_normal(unsigned long long seed, unsigned long long goff, int step, int B, float* out,
                                 hipStream_t s);
 hipError_t launch_posterior_stats(const float* x0, const int* tac, int B, int n_tac, int ncol,
@@ -105,8 +112,13 @@ hipError_t launch_posterior_stats(const float* x0, const int* tac, int B, int n_
 // Layer kinds of launch_conv (fixed shapes of the shipped config).
 enum LayerKind : int {
   LK_DOWN1 = 0, LK_DOWN2, LK_DOWN3, LK_UP0_CONV2, LK_UP0_BLOCK, LK_UP1_CONV2, LK_UP1_BLOCK,
-  LK_UP2_CONV2, LK_UP2_BLOCK, kNumConvLayers
+  LK_UP2_CONV2, LK_UP2_BLOCK, kNumConvLayers,
+  // Fused up levels (16-bit path): UpSampling1D -> Conv1D(k2) -> concat -> ConvBlock as ONE
+  // implicit GEMM.  The k2 conv is linear, so it composes with the block's k6 conv into a
+  // 2-phase (even / odd output position) 4-tap conv on the coarse input; see DESIGN.md.
+  LK_UP0_F = kNumConvLayers, LK_UP1_F, LK_UP2_F, kNumKinds
 };
+constexpr bool is_fused_kind(int kind) { return kind >= LK_UP0_F && kind < kNumKinds; }
 
 // Per-layer tile configuration, shared by the kernels and the host weight packer.
 //   wm x wn waves (wm*wn == 4): output tile (96*wm) rows x (64*wn) channels;
@@ -115,7 +127,7 @@ struct TileCfg {
   int wm, wn, stages, rowb;
 };
 constexpr TileCfg layer_tile(int kind) {
-  return kind == LK_UP2_BLOCK ? TileCfg{2, 2, 2, 64}          // final conv needs all 128 channels
+  return (kind == LK_UP2_BLOCK || kind == LK_UP2_F) ? TileCfg{2, 2, 2, 64}   // final conv needs all 128 channels
          : (kind == LK_UP0_CONV2 || kind == LK_UP1_CONV2 || kind == LK_UP2_CONV2) ? TileCfg{4, 1, 3, 128}
                                                                                   : TileCfg{4, 1, 3, 64};
 }

@@ -164,21 +164,29 @@ __device__ __forceinline__ void p_sample_elem(const FinalArgs& f, int t, float x
 // ---------------------------------------------------------------------------
 template <int KIND> struct LayerShape;
 //                                  L   UPS   TAPS PADL EPI
-template <> struct LayerShape<LK_DOWN1> { static constexpr int L = 24, TAPS = 6, PADL = 2, EPI = EPI_POOL; static constexpr bool UPS = false; };
-template <> struct LayerShape<LK_DOWN2> { static constexpr int L = 12, TAPS = 6, PADL = 2, EPI = EPI_POOL; static constexpr bool UPS = false; };
-template <> struct LayerShape<LK_DOWN3> { static constexpr int L = 6, TAPS = 6, PADL = 2, EPI = EPI_RELU; static constexpr bool UPS = false; };
-template <> struct LayerShape<LK_UP0_CONV2> { static constexpr int L = 12, TAPS = 2, PADL = 0, EPI = EPI_LIN; static constexpr bool UPS = true; };
-template <> struct LayerShape<LK_UP0_BLOCK> { static constexpr int L = 12, TAPS = 6, PADL = 2, EPI = EPI_RELU; static constexpr bool UPS = false; };
-template <> struct LayerShape<LK_UP1_CONV2> { static constexpr int L = 24, TAPS = 2, PADL = 0, EPI = EPI_LIN; static constexpr bool UPS = true; };
-template <> struct LayerShape<LK_UP1_BLOCK> { static constexpr int L = 24, TAPS = 6, PADL = 2, EPI = EPI_RELU; static constexpr bool UPS = false; };
-template <> struct LayerShape<LK_UP2_CONV2> { static constexpr int L = 48, TAPS = 2, PADL = 0, EPI = EPI_LIN; static constexpr bool UPS = true; };
-template <> struct LayerShape<LK_UP2_BLOCK> { static constexpr int L = 48, TAPS = 6, PADL = 2, EPI = EPI_FINAL; static constexpr bool UPS = false; };
+template <> struct LayerShape<LK_DOWN1> { static constexpr int L = 24, TAPS = 6, PADL = 2, EPI = EPI_POOL; static constexpr bool UPS = false, FUSED = false; };
+template <> struct LayerShape<LK_DOWN2> { static constexpr int L = 12, TAPS = 6, PADL = 2, EPI = EPI_POOL; static constexpr bool UPS = false, FUSED = false; };
+template <> struct LayerShape<LK_DOWN3> { static constexpr int L = 6, TAPS = 6, PADL = 2, EPI = EPI_RELU; static constexpr bool UPS = false, FUSED = false; };
+template <> struct LayerShape<LK_UP0_CONV2> { static constexpr int L = 12, TAPS = 2, PADL = 0, EPI = EPI_LIN; static constexpr bool UPS = true, FUSED = false; };
+template <> struct LayerShape<LK_UP0_BLOCK> { static constexpr int L = 12, TAPS = 6, PADL = 2, EPI = EPI_RELU; static constexpr bool UPS = false, FUSED = false; };
+template <> struct LayerShape<LK_UP1_CONV2> { static constexpr int L = 24, TAPS = 2, PADL = 0, EPI = EPI_LIN; static constexpr bool UPS = true, FUSED = false; };
+template <> struct LayerShape<LK_UP1_BLOCK> { static constexpr int L = 24, TAPS = 6, PADL = 2, EPI = EPI_RELU; static constexpr bool UPS = false, FUSED = false; };
+template <> struct LayerShape<LK_UP2_CONV2> { static constexpr int L = 48, TAPS = 2, PADL = 0, EPI = EPI_LIN; static constexpr bool UPS = true, FUSED = false; };
+template <> struct LayerShape<LK_UP2_BLOCK> { static constexpr int L = 48, TAPS = 6, PADL = 2, EPI = EPI_FINAL; static constexpr bool UPS = false, FUSED = false; };
+// Fused up levels: segment 1 = the skip s (L rows per sample, the block's 6 taps),
+// segment 2 = the coarse input b (L/2 rows per sample, 2 phases x 4 composite taps).
+template <> struct LayerShape<LK_UP0_F> { static constexpr int L = 12, TAPS = 6, PADL = 2, EPI = EPI_RELU; static constexpr bool UPS = false, FUSED = true; };
+template <> struct LayerShape<LK_UP1_F> { static constexpr int L = 24, TAPS = 6, PADL = 2, EPI = EPI_RELU; static constexpr bool UPS = false, FUSED = true; };
+template <> struct LayerShape<LK_UP2_F> { static constexpr int L = 48, TAPS = 6, PADL = 2, EPI = EPI_FINAL; static constexpr bool UPS = false, FUSED = true; };
+
+// launch-bound threads: 8 waves (4 MFMA + 4 loader) or 4 (fused layers)
+template <int KIND> constexpr int conv_max_threads() { return is_fused_kind(KIND) ? kThreads : 2 * kThreads; }
 
 template <typename T, int KIND>
 struct ConvGeom {
   using Sh = LayerShape<KIND>;
   static constexpr int L = Sh::L, TAPS = Sh::TAPS, PADL = Sh::PADL, EPI = Sh::EPI;
-  static constexpr bool UPS = Sh::UPS;
+  static constexpr bool UPS = Sh::UPS, FUSED = Sh::FUSED;
   static constexpr TileCfg TC = layer_tile(KIND);
   static constexpr int WM = TC.wm, WN = TC.wn, STAGES = TC.stages, ROWB = TC.rowb;
   static constexpr int MT = 96 * WM, NT = 64 * WN;
@@ -189,14 +197,29 @@ struct ConvGeom {
   static constexpr int CPR = ROWB / 16;             // 16-B pieces per LDS row
   static constexpr int KC = ROWB / (int)sizeof(T);  // input channels per chunk
   static constexpr int EPC = 16 / (int)sizeof(T);   // elements per 16-B piece
-  static constexpr int A_BYTES = ((AROWS + 1) * ROWB + 255) / 256 * 256;
+  static constexpr int A_BYTES = ((AROWS + (FUSED ? 0 : 1)) * ROWB + 255) / 256 * 256;
   static constexpr int B_BYTES = TAPS * NT * ROWB;
-  static constexpr int STAGE = A_BYTES + B_BYTES;
+  // Fused up levels, segment 2 (coarse input b): A = S * L/2 rows, B = [phase][4 taps][NT][ROWB].
+  // A stage holds either segment's layout; the zero row sits past both (ZOFF).
+  static constexpr int LH = L / 2;
+  static constexpr int AROWS2 = FUSED ? S * LH : 0;
+  static constexpr int TAPS2 = 4;
+  static constexpr int A2_BYTES = (AROWS2 * ROWB + 255) / 256 * 256;
+  static constexpr int B2_BYTES = FUSED ? 2 * TAPS2 * NT * ROWB : 0;
+  static constexpr int DATA = (A_BYTES + B_BYTES) > (A2_BYTES + B2_BYTES) ? A_BYTES + B_BYTES : A2_BYTES + B2_BYTES;
+  static constexpr int ZOFF = FUSED ? DATA : ZROW * ROWB;    // byte offset of the zero row in a stage
+  static constexpr int STAGE = FUSED ? (DATA + ROWB + 255) / 256 * 256 : A_BYTES + B_BYTES;
   static constexpr int APIECES = AROWS * CPR;
   static constexpr int APT = (APIECES + kThreads - 1) / kThreads;
   static constexpr int BPT = B_BYTES / 16 / kThreads;
   static constexpr bool AFULL = (APIECES % kThreads) == 0;
   static constexpr int PER = APT + BPT;             // LDS-DMA instructions per wave per chunk
+  static constexpr int APIECES2 = AROWS2 * CPR;
+  static constexpr int APT2 = (APIECES2 + kThreads - 1) / kThreads;
+  static constexpr int BPT2 = B2_BYTES / 16 / kThreads;
+  static constexpr bool AFULL2 = (APIECES2 % kThreads) == 0;
+  static constexpr int PER2 = APT2 + BPT2;          // segment-2 chunks
+  static constexpr int PHROWS = FUSED ? S * LH : MT; // tile rows per output phase (fused)
   static constexpr int CT_LD = 2 * NT + 8;          // fp32 C tile, one ROW PAIR [c][2] per line (non-final)
   static constexpr int FIN_LD = 132;                // fp32 C tile row (final epilogue, 16-B aligned)
   // FINAL: C tile | final kernel [128][4] | x_next rows [MT][2] (fused next-step down0)
@@ -219,19 +242,37 @@ struct ConvGeom {
   static_assert(!PREMAP || EPI_BYTES <= RING, "C tile must not overlap the prefetched maps");
   // Dedicated loader waves (16-bit 3-stage layers): 4 extra waves issue every LDS-DMA
   // piece, so the 4 MFMA waves never stall on DMA issue.
-  static constexpr bool LDR = CONV_LOADERS && sizeof(T) == 2 && STAGES == 3;
+  // (not the fused layers: 4 waves per workgroup leave them the whole 512-entry register file
+  // for the second segment's offsets and the correction weights)
+  static constexpr bool LDR = CONV_LOADERS && sizeof(T) == 2 && STAGES == 3 && !FUSED;
   static constexpr int NTH = LDR ? 2 * kThreads : kThreads;
   static_assert(WM * WN == 4, "4 waves");
   static_assert(MT % L == 0, "tile must hold whole samples");
   static_assert(B_BYTES % (16 * kThreads) == 0, "B tile split");
   static_assert(ROWB == 64 || ROWB == 128, "row width");
-  static_assert(STAGES == 2 || (STAGES == 3 && AFULL), "3-stage ring needs uniform per-wave DMA counts");
-  static_assert(PER < 64, "vmcnt range");
+  static_assert(STAGES == 2 || (STAGES == 3 && AFULL && AFULL2), "3-stage ring needs uniform per-wave DMA counts");
+  static_assert(PER < 64 && PER2 < 64, "vmcnt range");
+  static_assert(!FUSED || (PHROWS % 96 == 0 && S % 2 == 0 && S <= 32 && B2_BYTES % (16 * kThreads) == 0),
+                "fused: one output phase per wave, the m = 0 rows inside a wave's first fragment");
+  static_assert(!FUSED || sizeof(T) == 2, "fused layers: 16-bit MFMA path");
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   static_assert(EPI != EPI_FINAL || NT == 128, "final conv needs every channel in the tile");
   // XOR key of the 16-B piece index within a row: conflict-free ds_read_b128 for
   // 16 consecutive rows (lane groups of MI355X_MICROARCH.md LDS table)
   static __device__ __forceinline__ int key(int row) { return CPR == 4 ? ((row >> 2) & 3) : ((row >> 1) & 7); }
+  // tile row r -> (sample s, position l).  Fused tiles order their rows [phase e][m][sample]
+  // (l = 2m + e), so every wave computes one output phase and the m = 0 rows (the only ones
+  // whose composite taps need the left-edge correction) fill the first S rows of a phase.
+  static __device__ __forceinline__ void row_sl(int r, int& s, int& l) {
+    if constexpr (FUSED) {
+      s = r % S;
+      const int em = r / S, e = em / LH;
+      l = 2 * (em - e * LH) + e;
+    } else {
+      s = r / L;
+      l = r - s * L;
+    }
+  }
 };
 
 // Global -> LDS staging by LDS-DMA (global_load_lds_dwordx4).  Piece p of a
@@ -263,6 +304,7 @@ struct DmaPlan {
   using G = ConvGeom<T, KIND>;
   i32x4 rs1, rs2, rsw;                // buffer resources: src1, src2, packed weights
   int avoff1[G::APT], avoff2[G::APT]; // byte offsets of this lane's A pieces (chunk 0) in src1 / src2
+  int avoffh[G::APT2 > 0 ? G::APT2 : 1];  // fused segment 2: A pieces of the coarse input (src2)
   int bvoff;                          // byte offset of this lane's B piece 0 within a chunk's B tile
   int n1, wv, wbase;                  // wbase: byte offset of this tile's chunk 0 in the packed weights
 
@@ -270,26 +312,68 @@ struct DmaPlan {
     n1 = a.c1 / G::KC;
     wv = wv_;
     const unsigned rows = (unsigned)a.B * G::LIN;
+    const unsigned rows2 = G::FUSED ? (unsigned)a.B * G::LH : rows;
     rs1 = make_rsrc(a.src1, rows * (unsigned)a.c1 * (unsigned)sizeof(T));
-    rs2 = make_rsrc(a.src2 ? a.src2 : a.src1, rows * (unsigned)a.c2 * (unsigned)sizeof(T));
-    rsw = make_rsrc(a.wpack, (unsigned)(a.cout / G::NT) * (unsigned)NC * (unsigned)G::B_BYTES);
+    rs2 = make_rsrc(a.src2 ? a.src2 : a.src1, rows2 * (unsigned)a.c2 * (unsigned)sizeof(T));
+    const int tile_bytes = G::FUSED ? n1 * G::B_BYTES + (NC - n1) * G::B2_BYTES : NC * G::B_BYTES;
+    rsw = make_rsrc(a.wpack, (unsigned)(a.cout / G::NT) * (unsigned)tile_bytes);
 #pragma unroll
     for (int qq = 0; qq < G::APT; ++qq) {
       int p = qq * kThreads + wv * 64 + lane;
       if (p >= G::APIECES) p = G::APIECES - 1;   // inactive lanes of a partial last instruction
       const int row = p / G::CPR, cp = p - row * G::CPR;
       const int c = cp ^ G::key(row);
-      const int s = row / G::LIN, li = row - s * G::LIN;
+      // LDS row: (sample, position) = row / LIN, row % LIN; fused: position-major slots
+      // (row = li * S + s), so a lane group's 16 samples read 16 consecutive rows
+      const int s = G::FUSED ? row % G::S : row / G::LIN;
+      const int li = G::FUSED ? row / G::S : row - s * G::LIN;
       const int b = min(m0 + s, a.B - 1);        // rows of absent samples only feed unstored outputs
       avoff1[qq] = ((b * G::LIN + li) * a.c1 + c * G::EPC) * (int)sizeof(T);
       avoff2[qq] = ((b * G::LIN + li) * a.c2 + c * G::EPC) * (int)sizeof(T);
     }
+    if constexpr (G::FUSED) {
+#pragma unroll
+      for (int qq = 0; qq < G::APT2; ++qq) {
+        int p = qq * kThreads + wv * 64 + lane;
+        if (p >= G::APIECES2) p = G::APIECES2 - 1;
+        const int row = p / G::CPR, cp = p - row * G::CPR;
+        const int c = cp ^ G::key(row);
+        const int s = row % G::S, li = row / G::S;
+        const int b = min(m0 + s, a.B - 1);
+        avoffh[qq] = ((b * G::LH + li) * a.c2 + c * G::EPC) * (int)sizeof(T);
+      }
+    }
     bvoff = (wv * 64 + lane) * 16;
-    wbase = n_tile * NC * G::B_BYTES;
+    wbase = n_tile * tile_bytes;
   }
 
-  // issue DMA piece k (0..PER-1) of chunk kc into stage sbase
+  // pieces per wave of chunk kc (fused: segment 2 chunks differ)
+  __device__ __forceinline__ int per(int kc) const { return (G::FUSED && kc >= n1) ? G::PER2 : G::PER; }
+
+  // issue DMA piece k (0..per(kc)-1) of chunk kc into stage sbase
   __device__ __forceinline__ void piece(char* sbase, int k, int kc, int lane) const {
+    if (G::FUSED && kc >= n1) piece2(sbase, k, kc - n1, lane);
+    else piece1(sbase, k, kc, lane);
+  }
+  // fused segment-2 chunk k2 (coarse input b, both phases' composite taps)
+  __device__ __forceinline__ void piece2(char* sbase, int k, int k2, int lane) const {
+    if constexpr (G::FUSED) {
+      if (k < G::APT2) {
+        const int p0 = k * kThreads + wv * 64;
+        if (G::AFULL2 || p0 + lane < G::APIECES2)
+          llvm_amdgcn_raw_buffer_load_lds(rs2, (__attribute__((address_space(3))) void*)(sbase + p0 * 16), 16,
+                                          avoffh[k], k2 * G::KC * (int)sizeof(T), 0, 0);
+      } else {
+        const int qq = k - G::APT2;
+        const int p0 = qq * kThreads + wv * 64;
+        llvm_amdgcn_raw_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(sbase + G::A2_BYTES + p0 * 16),
+                                        16, bvoff + qq * kThreads * 16,
+                                        wbase + n1 * G::B_BYTES + k2 * G::B2_BYTES, 0, 0);
+      }
+    }
+  }
+  // a non-fused chunk, or a fused segment-1 chunk (kc < n1)
+  __device__ __forceinline__ void piece1(char* sbase, int k, int kc, int lane) const {
     if (k < G::APT) {
       const int p0 = k * kThreads + wv * 64;
       if (G::AFULL || p0 < G::APIECES) {
@@ -309,8 +393,13 @@ struct DmaPlan {
   }
 
   __device__ __forceinline__ void all(char* smem, int kc, int buf, int lane) const {
+    if (G::FUSED && kc >= n1) {
 #pragma unroll
-    for (int k = 0; k < G::PER; ++k) piece(smem + buf * G::STAGE, k, kc, lane);
+      for (int k = 0; k < G::PER2; ++k) piece(smem + buf * G::STAGE, k, kc, lane);
+    } else {
+#pragma unroll
+      for (int k = 0; k < G::PER; ++k) piece(smem + buf * G::STAGE, k, kc, lane);
+    }
   }
 };
 
@@ -439,7 +528,7 @@ __device__ __forceinline__ void ring_barrier() {
 }
 
 template <typename T, int KIND>
-__global__ __launch_bounds__(2 * kThreads, 1) void conv_kernel(ConvArgs<T> a) {
+__global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvArgs<T> a) {
   using G = ConvGeom<T, KIND>;
   constexpr int L = G::L, TAPS = G::TAPS, PADL = G::PADL, EPI = G::EPI, ROWB = G::ROWB, NT = G::NT;
   constexpr bool UPS = G::UPS;
@@ -488,7 +577,7 @@ __global__ __launch_bounds__(2 * kThreads, 1) void conv_kernel(ConvArgs<T> a) {
   // zero row of every stage
   if (tid < G::STAGES * G::CPR) {
     const int st = tid / G::CPR, pc = tid - st * G::CPR;
-    *reinterpret_cast<uint4*>(smem + st * G::STAGE + G::ZROW * ROWB + pc * 16) = make_uint4(0, 0, 0, 0);
+    *reinterpret_cast<uint4*>(smem + st * G::STAGE + G::ZOFF + pc * 16) = make_uint4(0, 0, 0, 0);
   }
 
   // per-lane LDS byte offsets of the A fragment rows (tap j, m-subtile i) and B rows
@@ -499,12 +588,14 @@ __global__ __launch_bounds__(2 * kThreads, 1) void conv_kernel(ConvArgs<T> a) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const int r = wm * 96 + i * 32 + lr;
-      const int s = r / L, l = r - s * L;
+      int s, l;
+      G::row_sl(r, s, l);
       const int p = l + j - PADL;
       int row;
-      if (!UPS) row = (p >= 0 && p < L) ? s * L + p : G::ZROW;
+      if (G::FUSED) row = (p >= 0 && p < L) ? p * G::S + s : G::ZROW;
+      else if (!UPS) row = (p >= 0 && p < L) ? s * L + p : G::ZROW;
       else row = (p < L) ? s * G::LIN + (p >> 1) : G::ZROW;
-      aoff[j][i] = row * ROWB + ((c0 ^ G::key(row)) << 4);
+      aoff[j][i] = (G::FUSED && row == G::ZROW) ? G::ZOFF + (c0 << 4) : row * ROWB + ((c0 ^ G::key(row)) << 4);
     }
   }
   int boff[2];
@@ -512,6 +603,35 @@ __global__ __launch_bounds__(2 * kThreads, 1) void conv_kernel(ConvArgs<T> a) {
   for (int jn = 0; jn < 2; ++jn) {
     const int n = wn * 64 + jn * 32 + lr;
     boff[jn] = G::A_BYTES + n * ROWB + ((c0 ^ G::key(n)) << 4);
+  }
+  // Fused segment 2: composite tap k of output row (s, l = 2m + e) reads coarse row m - 1 + k;
+  // B holds both phases' taps, a wave reads its own phase's.  The m = 0 rows also take the
+  // left-edge correction (amask: coarse row 0, registers epk), only in a wave's fragment 0.
+  constexpr int A2N = G::FUSED ? G::TAPS2 : 1;
+  int aoff2[A2N][3], boff2[2], amask = 0;
+  const int ph = G::FUSED ? (wm * 96) / G::PHROWS : 0;
+  const bool has_m0 = G::FUSED && (wm * 96) % G::PHROWS == 0;
+  if constexpr (G::FUSED) {
+#pragma unroll
+    for (int k = 0; k < G::TAPS2; ++k) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int r = wm * 96 + i * 32 + lr;
+        const int sq = r % G::S, m = (r / G::S) % G::LH, q = m - 1 + k;
+        const int row = q * G::S + sq;
+        aoff2[k][i] = (q >= 0 && q < G::LH) ? row * ROWB + ((c0 ^ G::key(row)) << 4) : G::ZOFF + (c0 << 4);
+      }
+    }
+    {
+      const int r = wm * 96 + lr;
+      const int sq = r % G::S, m = (r / G::S) % G::LH, row = sq;
+      amask = m == 0 ? row * ROWB + ((c0 ^ G::key(row)) << 4) : G::ZOFF + (c0 << 4);
+    }
+#pragma unroll
+    for (int jn = 0; jn < 2; ++jn) {
+      const int n = wn * 64 + jn * 32 + lr;
+      boff2[jn] = G::A2_BYTES + (ph * G::TAPS2 * NT + n) * ROWB + ((c0 ^ G::key(n)) << 4);
+    }
   }
   const int wv = __builtin_amdgcn_readfirstlane(w);
 
@@ -556,26 +676,58 @@ __global__ __launch_bounds__(2 * kThreads, 1) void conv_kernel(ConvArgs<T> a) {
         if constexpr (sizeof(T) == 2 && !(CONV_EXP_MODE & 2))
           acc[i][jn] = mfma32(av[pb][i], bv[pb][jn], acc[i][jn]);
   };
+  // Fused: left-edge correction weights of this lane (registers, one chunk ahead), see has_m0
+  constexpr int NGE = G::FUSED ? ROWB / 32 : 1;
+  fragT epk[NGE][2];
+#pragma unroll
+  for (int g = 0; g < NGE; ++g) epk[g][0] = epk[g][1] = fragT{};
+  const char* ebase = nullptr;
+  if constexpr (G::FUSED) {
+    const int n2 = a.c2 / G::KC;
+    ebase = reinterpret_cast<const char*>(a.epack) +
+            ((size_t)n_tile * n2 * 2 * NT + (size_t)ph * NT + wn * 64 + lr) * ROWB + h * 16;
+  }
+  auto load_epk = [&](int kc2) {   // segment-2 chunk kc2's correction fragments
+    if constexpr (G::FUSED) {
+      const char* p = ebase + (size_t)kc2 * 2 * NT * ROWB;
+#pragma unroll
+      for (int g = 0; g < NGE; ++g)
+#pragma unroll
+        for (int jn = 0; jn < 2; ++jn) epk[g][jn] = *reinterpret_cast<const fragT*>(p + jn * 32 * ROWB + g * 32);
+    }
+  };
   // NEXT = 2 (first chunk only): the pieces of chunks nkc and nkc + 1 (stages nbuf, nbuf + 1).
-  auto compute = [&](const char* base, auto next_tag, int nkc, int nbuf) {
+  // SEG = 2: a fused segment-2 chunk (4 composite taps of this wave's phase; kc = its index).
+  auto compute = [&](const char* base, auto next_tag, int nkc, int nbuf, auto seg_tag, int kc) {
     constexpr int NEXT = (int)decltype(next_tag)::value;
+    constexpr int SEG = (int)decltype(seg_tag)::value;
     char* nbase = smem + nbuf * G::STAGE;
     if constexpr (sizeof(T) == 2) {
       constexpr int NG = ROWB / 32;
-      constexpr int NS = TAPS * NG;
-      constexpr int NPC = (NEXT == 2 ? 2 : 1) * G::PER;   // pieces to issue over this chunk
+      constexpr int NT_ = SEG == 2 ? G::TAPS2 : TAPS;
+      constexpr int NS = NT_ * NG;
+      // NEXT: 0 none, 1 the next chunk, 2 the next two chunks, 3 the next chunk, a fused segment-2 one
+      constexpr int NPER = NEXT == 3 ? G::PER2 : G::PER;
+      constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;     // pieces to issue over this chunk
       constexpr int PPS = (NPC + NS - 1) / NS;            // DMA pieces per step
       static_assert(NS % 2 == 0, "fragment double buffer alternates per step");
+      fragT am[SEG == 2 ? NG : 1];
 #pragma unroll
       for (int st = 0; st < NS; ++st) {
         const int j = st / NG, g = st % NG, sb = st & 1;
         // interleave one fragment read per MFMA gap, in the order the next step's
         // MFMAs consume them (A0 B0 B1 A1 A2); each (MFMA, read) pair is pinned
-        const char* pa0 = base + (aoff[j][0] ^ (g << 5));
-        const char* pa1 = base + (aoff[j][1] ^ (g << 5));
-        const char* pa2 = base + (aoff[j][2] ^ (g << 5));
-        const char* pb0 = base + ((boff[0] + j * NT * ROWB) ^ (g << 5));
-        const char* pb1 = base + ((boff[1] + j * NT * ROWB) ^ (g << 5));
+        int ao0, ao1, ao2, bo0, bo1;
+        if constexpr (SEG == 2) {
+          ao0 = aoff2[j][0]; ao1 = aoff2[j][1]; ao2 = aoff2[j][2]; bo0 = boff2[0]; bo1 = boff2[1];
+        } else {
+          ao0 = aoff[j][0]; ao1 = aoff[j][1]; ao2 = aoff[j][2]; bo0 = boff[0]; bo1 = boff[1];
+        }
+        const char* pa0 = base + (ao0 ^ (g << 5));
+        const char* pa1 = base + (ao1 ^ (g << 5));
+        const char* pa2 = base + (ao2 ^ (g << 5));
+        const char* pb0 = base + ((bo0 + j * NT * ROWB) ^ (g << 5));
+        const char* pb1 = base + ((bo1 + j * NT * ROWB) ^ (g << 5));
         const int pb = sb ^ 1;
 #define PETDIFF_MF(i, jn)                                                                                  \
   if constexpr (!(CONV_EXP_MODE & 2))                                                                      \
@@ -600,12 +752,33 @@ __global__ __launch_bounds__(2 * kThreads, 1) void conv_kernel(ConvArgs<T> a) {
         PETDIFF_MF(2, 1)
 #undef PETDIFF_RD
 #undef PETDIFF_MF
+        if constexpr (SEG == 2) {
+          // left-edge correction of the m = 0 rows: coarse row 0 x (-K W1) (registers), read
+          // after step 0's reads, multiplied after step 1's MFMAs; then the next chunk's weights
+          if (st == 0 && has_m0) {
+#pragma unroll
+            for (int gg = 0; gg < NG; ++gg) am[gg] = *reinterpret_cast<const fragT*>(base + (amask ^ (gg << 5)));
+          }
+          if (st == 1 && has_m0) {
+#pragma unroll
+            for (int gg = 0; gg < NG; ++gg)
+#pragma unroll
+              for (int jn = 0; jn < 2; ++jn)
+                if constexpr (!(CONV_EXP_MODE & 2)) acc[0][jn] = mfma32(am[gg], epk[gg][jn], acc[0][jn]);
+            const int k2 = kc - dma.n1;
+            if (kc + 1 < NC) load_epk(k2 + 1);
+          }
+        }
         if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
 #pragma unroll
           for (int u = 0; u < PPS; ++u) {
             const int k = st * PPS + u;
-            if (k < G::PER) dma.piece(nbase, k, nkc, lane);
-            else if (k < NPC) dma.piece(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
+            if (k < NPER) {
+              if constexpr (NEXT == 3) dma.piece2(nbase, k, nkc - dma.n1, lane);
+              else dma.piece1(nbase, k, nkc, lane);
+            } else if (NEXT == 2 && k < NPC) {
+              dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
+            }
           }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -702,17 +875,75 @@ __global__ __launch_bounds__(2 * kThreads, 1) void conv_kernel(ConvArgs<T> a) {
 #if CONV_EXP_MODE & 128
   unsigned long long st_c0 = 0, st_r0 = 0;
 #endif
-  if constexpr (G::STAGES == 2) {
+  using Seg1 = std::integral_constant<int, 1>;
+  using Seg2 = std::integral_constant<int, 2>;
+  using Seg2Next = std::integral_constant<int, 3>;
+  if constexpr (G::FUSED) {
+    // Fused up level: segment-1 chunks (skip s), then segment-2 chunks (coarse b); every
+    // compute has its own and its DMA target's segment at compile time, so no loop body
+    // branches on the segment.  Host guarantees n1 >= 3 (3-stage) / >= 1 and n2 >= 2.
+    const int n1 = dma.n1;
+    if (has_m0) load_epk(0);   // the first segment-2 chunk's correction weights
+    if constexpr (G::STAGES == 2) {
+      dma.all(smem, 0, 0, lane);
+      prefetch_maps();
+      wait_vmcnt<0>();
+      __syncthreads();
+      int kc = 0;
+      for (; kc + 1 < n1; ++kc) {
+        compute(smem + (kc & 1) * G::STAGE, Yes{}, kc + 1, (kc + 1) & 1, Seg1{}, 0);
+        wait_vmcnt<0>();
+        __syncthreads();
+      }
+      compute(smem + (kc & 1) * G::STAGE, Seg2Next{}, kc + 1, (kc + 1) & 1, Seg1{}, 0);
+      wait_vmcnt<0>();
+      __syncthreads();
+      for (++kc; kc + 1 < NC; ++kc) {
+        compute(smem + (kc & 1) * G::STAGE, Seg2Next{}, kc + 1, (kc + 1) & 1, Seg2{}, kc);
+        wait_vmcnt<0>();
+        __syncthreads();
+      }
+      compute(smem + (kc & 1) * G::STAGE, No{}, 0, 0, Seg2{}, kc);
+      __syncthreads();
+    } else {
+      dma.all(smem, 0, 0, lane);
+      prefetch_maps();
+      ring_barrier<0>();
+      compute(smem, Two{}, 1, 1, Seg1{}, 0);              // chunks 1, 2 -> stages 1, 2
+      ring_barrier<G::PER>();
+      int buf = 1, kc = 1;
+      for (; kc + 2 < n1; ++kc) {
+        compute(smem + buf * G::STAGE, Yes{}, kc + 2, buf == 0 ? 2 : buf - 1, Seg1{}, 0);
+        ring_barrier<G::PER>();
+        buf = buf == 2 ? 0 : buf + 1;
+      }
+      for (; kc < n1; ++kc) {                              // the next chunks are segment 2
+        compute(smem + buf * G::STAGE, Seg2Next{}, kc + 2, buf == 0 ? 2 : buf - 1, Seg1{}, 0);
+        ring_barrier<G::PER2>();
+        buf = buf == 2 ? 0 : buf + 1;
+      }
+      for (; kc + 2 < NC; ++kc) {
+        compute(smem + buf * G::STAGE, Seg2Next{}, kc + 2, buf == 0 ? 2 : buf - 1, Seg2{}, kc);
+        ring_barrier<G::PER2>();
+        buf = buf == 2 ? 0 : buf + 1;
+      }
+      compute(smem + buf * G::STAGE, No{}, 0, 0, Seg2{}, kc);
+      ring_barrier<0>();
+      buf = buf == 2 ? 0 : buf + 1;
+      compute(smem + buf * G::STAGE, No{}, 0, 0, Seg2{}, kc + 1);
+      ring_barrier<0>();
+    }
+  } else if constexpr (G::STAGES == 2) {
     dma.all(smem, 0, 0, lane);
     prefetch_maps();
     wait_vmcnt<0>();
     __syncthreads();
     for (int kc = 0; kc + 1 < NC; ++kc) {
-      compute(smem + (kc & 1) * G::STAGE, Yes{}, kc + 1, (kc + 1) & 1);
+      compute(smem + (kc & 1) * G::STAGE, Yes{}, kc + 1, (kc + 1) & 1, Seg1{}, 0);
       wait_vmcnt<0>();
       __syncthreads();
     }
-    compute(smem + ((NC - 1) & 1) * G::STAGE, No{}, 0, 0);
+    compute(smem + ((NC - 1) & 1) * G::STAGE, No{}, 0, 0, Seg1{}, 0);
     __syncthreads();
   } else {
     // 3-deep ring: chunk kc+2 is in flight while chunk kc is computed; the wait
@@ -739,7 +970,7 @@ __global__ __launch_bounds__(2 * kThreads, 1) void conv_kernel(ConvArgs<T> a) {
 #endif
       int buf = 0;
       for (int kc = 0; kc < NC; ++kc) {
-        compute(smem + buf * G::STAGE, No{}, 0, 0);
+        compute(smem + buf * G::STAGE, No{}, 0, 0, Seg1{}, 0);
         ring_barrier<0>();                                 // B(kc+1): own LDS reads done
         buf = buf == 2 ? 0 : buf + 1;
       }
@@ -767,10 +998,10 @@ __global__ __launch_bounds__(2 * kThreads, 1) void conv_kernel(ConvArgs<T> a) {
     int buf = 0, kc = 0;
     if constexpr (EARLY) {
       if (NC >= 3) {
-        compute(smem, Two{}, 1, 1);                    // chunks 1, 2 -> stages 1, 2
+        compute(smem, Two{}, 1, 1, Seg1{}, 0);                    // chunks 1, 2 -> stages 1, 2
         ring_barrier<G::PER>();
       } else if (NC == 2) {
-        compute(smem, Yes{}, 1, 1);
+        compute(smem, Yes{}, 1, 1, Seg1{}, 0);
         ring_barrier<0>();
       }
       if (NC >= 2) {
@@ -780,18 +1011,18 @@ __global__ __launch_bounds__(2 * kThreads, 1) void conv_kernel(ConvArgs<T> a) {
     }
     for (; kc + 2 < NC; ++kc) {
       const int nb = buf == 0 ? 2 : buf - 1;          // (kc + 2) % 3
-      compute(smem + buf * G::STAGE, Yes{}, kc + 2, nb);
+      compute(smem + buf * G::STAGE, Yes{}, kc + 2, nb, Seg1{}, 0);
       ring_barrier<G::PER>();
       buf = buf == 2 ? 0 : buf + 1;
     }
     // tail: the last (up to) two chunks, nothing left to prefetch
     if (kc + 1 < NC) {
-      compute(smem + buf * G::STAGE, No{}, 0, 0);
+      compute(smem + buf * G::STAGE, No{}, 0, 0, Seg1{}, 0);
       ring_barrier<0>();
       buf = buf == 2 ? 0 : buf + 1;
     }
     if (kc < NC) {
-      compute(smem + buf * G::STAGE, No{}, 0, 0);
+      compute(smem + buf * G::STAGE, No{}, 0, 0, Seg1{}, 0);
       ring_barrier<0>();
     }
   }
@@ -859,8 +1090,11 @@ __global__ __launch_bounds__(2 * kThreads, 1) void conv_kernel(ConvArgs<T> a) {
       constexpr bool FAST = MODE != 0;
 #pragma unroll
     for (int rp = tid / TPR; rp < G::MT / 2; rp += kThreads / TPR) {
+      // the pair (r, r + 1): positions (l, l + 1) of sample s, or (fused) samples (s, s + 1) at l
       const int r = 2 * rp;
-      const int s = r / L, l = r - s * L, b = m0 + s;
+      int s, l;
+      G::row_sl(r, s, l);
+      const int b = m0 + s;
       if (!FAST && b >= B) continue;
       float v[2][8];
       f32x4 cq[4];   // (r, r+1) x channels nloc .. nloc+7, interleaved
@@ -868,24 +1102,26 @@ __global__ __launch_bounds__(2 * kThreads, 1) void conv_kernel(ConvArgs<T> a) {
       for (int k = 0; k < 4; ++k) cq[k] = *reinterpret_cast<const f32x4*>(ct + rp * G::CT_LD + nloc * 2 + 4 * k);
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
+        const int se = G::FUSED ? s + e : s, le = G::FUSED ? l : l + e, be = m0 + se;
+        if (G::FUSED && !FAST && be >= B) continue;
         const f32x4 c0v = {cq[0][e], cq[0][2 + e], cq[1][e], cq[1][2 + e]};
         const f32x4 c1v = {cq[2][e], cq[2][2 + e], cq[3][e], cq[3][2 + e]};
         f32x4 m0v = ep_b0, m1v = ep_b1;
         if constexpr (MODE == 1) {
-          m0v = *reinterpret_cast<const f32x4*>(lt + (l + e) * NT + nloc) +
-                *reinterpret_cast<const f32x4*>(lc + (l + e) * NT + nloc);
-          m1v = *reinterpret_cast<const f32x4*>(lt + (l + e) * NT + nloc + 4) +
-                *reinterpret_cast<const f32x4*>(lc + (l + e) * NT + nloc + 4);
+          m0v = *reinterpret_cast<const f32x4*>(lt + le * NT + nloc) +
+                *reinterpret_cast<const f32x4*>(lc + le * NT + nloc);
+          m1v = *reinterpret_cast<const f32x4*>(lt + le * NT + nloc + 4) +
+                *reinterpret_cast<const f32x4*>(lc + le * NT + nloc + 4);
         } else if constexpr (MODE == 0) {
-          const int tac = stac[s];
+          const int tac = stac[se];
           if (a.tmap) {
-            const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[b];
-            const float* mp = a.tmap + ((size_t)t * L + l + e) * cout + n;
+            const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[be];
+            const float* mp = a.tmap + ((size_t)t * L + le) * cout + n;
             m0v = *reinterpret_cast<const f32x4*>(mp);
             m1v = *reinterpret_cast<const f32x4*>(mp + 4);
           }
           if (a.cmap) {
-            const float* cp = a.cmap + ((size_t)tac * L + l + e) * cout + n;
+            const float* cp = a.cmap + ((size_t)tac * L + le) * cout + n;
             m0v += *reinterpret_cast<const f32x4*>(cp);
             m1v += *reinterpret_cast<const f32x4*>(cp + 4);
           }
@@ -899,7 +1135,7 @@ __global__ __launch_bounds__(2 * kThreads, 1) void conv_kernel(ConvArgs<T> a) {
 #pragma unroll
           for (int q = 0; q < 8; ++q) v[e][q] = fmaxf(v[e][q], 0.f);
         }
-        if (!FAST || b < B) Vec8<T>::store(a.out + ((size_t)b * L + l + e) * cout + n, v[e]);
+        if (!FAST || be < B) Vec8<T>::store(a.out + ((size_t)be * L + le) * cout + n, v[e]);
       }
       if constexpr (EPI == EPI_POOL) {
         float pv[8];
@@ -934,7 +1170,9 @@ __global__ __launch_bounds__(2 * kThreads, 1) void conv_kernel(ConvArgs<T> a) {
 #pragma unroll
         for (int rg = 0; rg < 16; ++rg) {
           const int r = wm * 96 + i * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * h;
-          fin[r * G::FIN_LD + wn * 64 + jn * 32 + lr] = acc[i][jn][rg];
+          int sr, lr_;
+          G::row_sl(r, sr, lr_);
+          fin[(sr * L + lr_) * G::FIN_LD + wn * 64 + jn * 32 + lr] = acc[i][jn][rg];
         }
     // final kernel as [n][4] (zero-padded when n_out == 2) for float4 reads
     for (int e = tid; e < 128 * 4; e += kThreads) {
@@ -1152,6 +1390,73 @@ __global__ void fold_map_kernel(const float* seq, int n, int Lseq, int Cs, const
   out[idx] = acc;
 }
 
+// Fused up level (DESIGN.md "fused up levels"): the UpSampling1D(2) -> Conv1D(k2, pad (0,1))
+// -> [skip | u] -> ConvBlock(k6 + res, pad (2,3)) chain is linear in u, so for output position
+// l = 2m + e the u-path is sum_k C_{e,k} b[m - 1 + k] over the coarse input b.  Composite
+// tap (e, k) = sum of K_j (alpha W0 + beta W1) over the terms below (K_j: the block kernel's
+// u rows, residual folded into j = 2; W_i: the k2 kernel's x rows).  Taps 8, 9: the left
+// edge, where the naive sum also counts u[-1] = W1 b[0] (a zero-padded position of the
+// block conv): the m = 0 rows add (-K1 W1) b[0] (even) / (-K0 W1) b[0] (odd).
+__constant__ int kCompJ[10][3] = {{0, 1, 0}, {1, 2, 3}, {3, 4, 5}, {5, 0, 0},
+                                  {0, 0, 0}, {0, 1, 2}, {2, 3, 4}, {4, 5, 0}, {1, 0, 0}, {0, 0, 0}};
+__constant__ float kCompA[10][3] = {{1, 1, 0}, {0, 1, 1}, {0, 1, 1}, {0, 0, 0},
+                                    {1, 0, 0}, {0, 1, 1}, {0, 1, 1}, {0, 1, 0}, {0, 0, 0}, {0, 0, 0}};
+__constant__ float kCompB[10][3] = {{1, 0, 0}, {1, 1, 0}, {1, 1, 0}, {1, 0, 0},
+                                    {0, 0, 0}, {1, 1, 0}, {1, 1, 0}, {1, 1, 0}, {-1, 0, 0}, {-1, 0, 0}};
+__constant__ int kCompN[10] = {2, 3, 3, 1, 1, 3, 3, 2, 1, 1};
+
+// out[tap][cb][o] = sum_terms sum_c (alpha W0[cb][c] + beta W1[cb][c]) * K_j[c][o]   (fp64 sums)
+__global__ void compose_kernel(const float* wup, int cin_up, int xoff, int cbn, int cu, const float* kblk,
+                               const float* kres, int cin_blk, int ch0, int cout, float* out) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)10 * cbn * cout) return;
+  const int o = (int)(idx % cout);
+  const int cb = (int)((idx / cout) % cbn);
+  const int tap = (int)(idx / ((size_t)cout * cbn));
+  const float* w0 = wup + (size_t)(xoff + cb) * cu;
+  const float* w1 = wup + (size_t)(cin_up + xoff + cb) * cu;
+  double acc = 0.0;
+  for (int q = 0; q < kCompN[tap]; ++q) {
+    const int j = kCompJ[tap][q];
+    const double al = kCompA[tap][q], be = kCompB[tap][q];
+    const float* kj = kblk + ((size_t)j * cin_blk + ch0) * cout + o;
+    const float* kr = kres + (size_t)ch0 * cout + o;
+    for (int c = 0; c < cu; ++c) {
+      double k = kj[(size_t)c * cout];
+      if (j == 2) k += kr[(size_t)c * cout];
+      acc += (al * w0[c] + be * w1[c]) * k;
+    }
+  }
+  out[idx] = (float)acc;
+}
+
+// The u-path's constant maps (k2 conv bias + its folded label / time channels, [n][L][cu])
+// through the block conv (zero padding of u), + the block biases: [n][L][cout].
+__global__ void map_through_kernel(const float* in, int n, int L, int cu, const float* kblk, const float* kres,
+                                   int taps, int padl, int cin_blk, int ch0, const float* b1, const float* b2,
+                                   float* out, int cout) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)n * L * cout) return;
+  const int o = (int)(idx % cout);
+  const int l = (int)((idx / cout) % L);
+  const int k = (int)(idx / ((size_t)cout * L));
+  double acc = 0.0;
+  for (int j = 0; j < taps; ++j) {
+    const int q = l + j - padl;
+    if (q < 0 || q >= L) continue;
+    const float* u = in + ((size_t)k * L + q) * cu;
+    const float* kj = kblk + ((size_t)j * cin_blk + ch0) * cout + o;
+    for (int c = 0; c < cu; ++c) {
+      double w = kj[(size_t)c * cout];
+      if (j == padl) w += kres[(size_t)(ch0 + c) * cout + o];
+      acc += w * u[c];
+    }
+  }
+  if (b1) acc += b1[o];
+  if (b2) acc += b2[o];
+  out[idx] = (float)acc;
+}
+
 // x_T ~ N(0, 1) from the same counter-based stream (step id = rng_step), so a
 // sharded run draws exactly the samples of the unsharded one.
 __global__ void philox_normal_kernel(unsigned long long seed, unsigned long long goff, int step, int B, float* out) {
@@ -1213,6 +1518,7 @@ static hipError_t launch_one(const ConvArgs<T>& a, hipStream_t s) {
   using G = ConvGeom<T, KIND>;
   if (a.B <= 0) return hipSuccess;
   if (a.cout % G::NT != 0 || a.c1 % G::KC != 0 || a.c2 % G::KC != 0) return hipErrorInvalidValue;
+  if (G::FUSED && (!a.src2 || !a.epack || a.c2 <= 0)) return hipErrorInvalidValue;
   const int nM = (a.B + G::S - 1) / G::S;
   const int total = nM * (a.cout / G::NT);
   hipLaunchKernelGGL((conv_kernel<T, KIND>), dim3(total), dim3(G::NTH), 0, s, a);
@@ -1231,6 +1537,13 @@ hipError_t launch_conv(int kind, const ConvArgs<T>& a, hipStream_t s) {
     case LK_UP1_BLOCK: return launch_one<T, LK_UP1_BLOCK>(a, s);
     case LK_UP2_CONV2: return launch_one<T, LK_UP2_CONV2>(a, s);
     case LK_UP2_BLOCK: return launch_one<T, LK_UP2_BLOCK>(a, s);
+  }
+  if constexpr (sizeof(T) == 2) {   // fused up levels: 16-bit MFMA path only
+    switch (kind) {
+      case LK_UP0_F: return launch_one<T, LK_UP0_F>(a, s);
+      case LK_UP1_F: return launch_one<T, LK_UP1_F>(a, s);
+      case LK_UP2_F: return launch_one<T, LK_UP2_F>(a, s);
+    }
   }
   return hipErrorInvalidValue;
 }
@@ -1273,6 +1586,24 @@ hipError_t launch_fold(const float* seq, int n, int Lseq, int Cs, const float* w
   if (tot == 0) return hipSuccess;
   hipLaunchKernelGGL(fold_map_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, seq, n, Lseq, Cs, wk,
                      taps, padl, ups, cin_full, ch0, wr, b1, b2, out, Lout, cout);
+  return hipGetLastError();
+}
+
+hipError_t launch_compose(const float* wup, int cin_up, int xoff, int cbn, int cu, const float* kblk,
+                          const float* kres, int cin_blk, int ch0, int cout, float* out, hipStream_t s) {
+  const size_t tot = (size_t)10 * cbn * cout;
+  hipLaunchKernelGGL(compose_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, wup, cin_up, xoff, cbn, cu,
+                     kblk, kres, cin_blk, ch0, cout, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_map_through(const float* in, int n, int L, int cu, const float* kblk, const float* kres, int taps,
+                              int padl, int cin_blk, int ch0, const float* b1, const float* b2, float* out, int cout,
+                              hipStream_t s) {
+  const size_t tot = (size_t)n * L * cout;
+  if (tot == 0) return hipSuccess;
+  hipLaunchKernelGGL(map_through_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, in, n, L, cu, kblk,
+                     kres, taps, padl, cin_blk, ch0, b1, b2, out, cout);
   return hipGetLastError();
 }
 

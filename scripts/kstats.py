@@ -4,13 +4,14 @@ import csv
 import re
 import sys
 
-LAYERS = ['down1', 'down2', 'down3', 'up0.conv2', 'up0.block', 'up1.conv2', 'up1.block', 'up2.conv2', 'up2.block']
+LAYERS = ['down1', 'down2', 'down3', 'up0.conv2', 'up0.block', 'up1.conv2', 'up1.block', 'up2.conv2', 'up2.block',
+          'up0.fused', 'up1.fused', 'up2.fused']
 
 
 def label(name):
     if 'down0_kernel' in name:
         return 'down0'
-    m = re.search(r'conv_kernel.*?Li(\d)E', name) or re.search(r'conv_kernel<[^,]*, (\d)>', name)
+    m = re.search(r'conv_kernel.*?Li(\d+)E', name) or re.search(r'conv_kernel<[^,]*, (\d+)>', name)
     if 'conv_kernel' in name:
         if m:
             return LAYERS[int(m.group(1))]

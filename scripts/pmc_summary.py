@@ -11,12 +11,13 @@ import sys
 from collections import defaultdict
 
 
-LAYERS = ['down1', 'down2', 'down3', 'up0.conv2', 'up0.block', 'up1.conv2', 'up1.block', 'up2.conv2', 'up2.block']
+LAYERS = ['down1', 'down2', 'down3', 'up0.conv2', 'up0.block', 'up1.conv2', 'up1.block', 'up2.conv2', 'up2.block',
+          'up0.fused', 'up1.fused', 'up2.fused']
 
 
 def short(name):
     import re
-    m = re.search(r'conv_kernelI(?:DF16b|f)Li(\d)E', name)
+    m = re.search(r'conv_kernelI(?:DF16b|f)Li(\d+)E', name)
     if m:
         return LAYERS[int(m.group(1))]
     if 'down0_kernel' in name:
@@ -43,14 +44,18 @@ def main(d, out=None):
         print(k, {c: round(v, 1) for c, v in res[k].items()})
     if out:
         json.dump(res, open(out, 'w'), indent=1)
-        ub = res.get('up0.block', {})
-        if 'hbm_read_bytes_corrected' in ub and 'hbm_write_bytes' in ub:
-            tr = {'up0_block_bytes_per_launch': ub['hbm_read_bytes_corrected'] + ub['hbm_write_bytes'],
-                  'read_bytes': ub['hbm_read_bytes_corrected'], 'write_bytes': ub['hbm_write_bytes'],
-                  'source': os.path.relpath(out, os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
-                  'method': 'rocprofv3 --pmc FETCH_SIZE (x2, gfx950 64-B tally) + WRITE_SIZE, KB->B, mean per dispatch'}
-            json.dump(tr, open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                                            'profiles', 'pmc_traffic.json'), 'w'), indent=1)
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        tp = os.path.join(root, 'profiles', 'pmc_traffic.json')
+        tr = json.load(open(tp)) if os.path.exists(tp) else {}
+        for key, pre in (('up0.block', 'up0_block'), ('up0.fused', 'up0_fused')):
+            ub = res.get(key, {})
+            if 'hbm_read_bytes_corrected' in ub and 'hbm_write_bytes' in ub:
+                tr[pre + '_bytes_per_launch'] = ub['hbm_read_bytes_corrected'] + ub['hbm_write_bytes']
+                tr[pre + '_read_bytes'] = ub['hbm_read_bytes_corrected']
+                tr[pre + '_write_bytes'] = ub['hbm_write_bytes']
+                tr[pre + '_source'] = os.path.relpath(out, root)
+        tr['method'] = 'rocprofv3 --pmc FETCH_SIZE (x2, gfx950 64-B tally) + WRITE_SIZE, KB->B, mean per dispatch'
+        json.dump(tr, open(tp, 'w'), indent=1)
     return res
 
 

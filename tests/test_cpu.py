@@ -288,3 +288,40 @@ def test_gloo_world2_allgather_merge():
         p.join(timeout=120)
         assert p.exitcode == 0
     assert np.abs(dm).max() < 1e-12 and np.abs(ds).max() < 1e-12
+
+
+def test_fused_up_composite_identity():
+    """The algebra behind the fused up levels (csrc/unet_kernels.hip compose_kernel):
+    UpSampling1D(2) -> Conv1D(k=2, 'same' = pad (0, 1)) -> concat -> Conv1D(k=6, 'same' = pad (2, 3))
+    (networks.py:970-975, 1046-1057, 679-691) equals, for output l = 2m + e, the 4-tap conv
+    sum_k C[e][k] b[m - 1 + k] on the coarse input, plus (-K1 W1) b[0] at l = 0 and (-K0 W1) b[0]
+    at l = 1, plus the k2 bias pushed through the zero-padded k6 conv.  Same term table as the kernel."""
+    rng = np.random.default_rng(0)
+    for Lh in (3, 6, 12):
+        L, cb, cu, co = 2 * Lh, 5, 4, 3
+        W = rng.standard_normal((2, cb, cu))
+        K = rng.standard_normal((6, cu, co))
+        bu = rng.standard_normal(cu)
+        b = rng.standard_normal((Lh, cb))
+        # direct: upsample, k2 conv (pad right 1), k6 conv over u (pad 2 left, 3 right)
+        v = np.repeat(b, 2, axis=0)
+        vp = np.concatenate([v, np.zeros((1, cb))])
+        u = vp[:L] @ W[0] + vp[1:L + 1] @ W[1] + bu
+        up = np.concatenate([np.zeros((2, cu)), u, np.zeros((3, cu))])
+        y = sum(up[j:j + L] @ K[j] for j in range(6))
+        # composite: term table (j, alpha, beta) of kCompJ / kCompA / kCompB
+        terms = [[(0, 1, 1), (1, 1, 0)], [(1, 0, 1), (2, 1, 1), (3, 1, 0)], [(3, 0, 1), (4, 1, 1), (5, 1, 0)],
+                 [(5, 0, 1)], [(0, 1, 0)], [(0, 0, 1), (1, 1, 1), (2, 1, 0)], [(2, 0, 1), (3, 1, 1), (4, 1, 0)],
+                 [(4, 0, 1), (5, 1, 1)], [(1, 0, -1)], [(0, 0, -1)]]
+        C = [sum((al * W[0] + be * W[1]) @ K[j] for j, al, be in tt) for tt in terms]
+        bp = np.concatenate([np.zeros((1, cb)), b, np.zeros((2, cb))])   # b[-1], b[Lh], b[Lh+1] = 0
+        # bias: u's constant part through the zero-padded k6 conv (map_through_kernel)
+        cst = np.concatenate([np.zeros((2, cu)), np.tile(bu, (L, 1)), np.zeros((3, cu))])
+        ybias = sum(cst[j:j + L] @ K[j] for j in range(6))
+        yc = np.empty_like(y)
+        for l in range(L):
+            m, e = divmod(l, 2)
+            yc[l] = sum(bp[m + k] @ C[4 * e + k] for k in range(4)) + ybias[l]
+            if m == 0:
+                yc[l] += b[0] @ C[8 + e]
+        np.testing.assert_allclose(yc, y, rtol=1e-12, atol=1e-12)
