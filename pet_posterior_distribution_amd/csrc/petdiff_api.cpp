@@ -169,6 +169,9 @@ struct petdiff_ctx {
 
 namespace {
 
+// XOR key of the 16-B piece index within a packed weight row n (= ConvGeom::key)
+int piece_key(int n, int cpr) { return cpr == 4 ? ((n >> 2) & 3) : cpr == 2 ? ((n >> 3) & 1) : ((n >> 1) & 7); }
+
 template <typename T, typename H>
 int pack_conv(petdiff_ctx* h, const std::vector<float>& wk_host, int li) {
   const ConvLayer& cl = kConv[li];
@@ -198,8 +201,7 @@ int pack_conv(petdiff_ctx* h, const std::vector<float>& wk_host, int li) {
       for (int j = 0; j < cl.taps; ++j)
         for (int n = 0; n < NT; ++n)
           for (int p = 0; p < CPR; ++p) {
-            const int key = CPR == 4 ? ((n >> 2) & 3) : ((n >> 1) & 7);
-            const int c = p ^ key;
+            const int c = p ^ piece_key(n, CPR);
             for (int e = 0; e < EPC; ++e) {
               const int ci = cl.xoff + kc * KC + c * EPC + e;
               const int co = nt * NT + n;
@@ -262,7 +264,7 @@ int pack_fused(petdiff_ctx* h, const std::vector<float>& host, int u) {
       for (int j = 0; j < 6; ++j)
         for (int n = 0; n < NT; ++n)
           for (int p = 0; p < CPR; ++p) {
-            const int c = p ^ ((n >> 2) & 3);
+            const int c = p ^ piece_key(n, CPR);
             for (int e = 0; e < EPC; ++e) {
               const int ci = kc * KC + c * EPC + e, co = nt * NT + n;
               float v = wk[((size_t)j * blk.cin_full + ci) * blk.cout + co];
@@ -274,7 +276,7 @@ int pack_fused(petdiff_ctx* h, const std::vector<float>& host, int u) {
       for (int t = 0; t < 8; ++t)
         for (int n = 0; n < NT; ++n)
           for (int p = 0; p < CPR; ++p) {
-            const int c = p ^ ((n >> 2) & 3);
+            const int c = p ^ piece_key(n, CPR);
             for (int e = 0; e < EPC; ++e) {
               const int cb = kc * KC + c * EPC + e, co = nt * NT + n;
               out[q++] = cvt(D[((size_t)t * fl.cb + cb) * fl.cout + co]);

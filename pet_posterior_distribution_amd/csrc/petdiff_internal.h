@@ -127,7 +127,8 @@ struct TileCfg {
   int wm, wn, stages, rowb;
 };
 constexpr TileCfg layer_tile(int kind) {
-  return (kind == LK_UP2_BLOCK || kind == LK_UP2_F) ? TileCfg{2, 2, 2, 64}   // final conv needs all 128 channels
+  return kind == LK_UP2_BLOCK ? TileCfg{2, 2, 2, 64}                // final conv needs all 128 channels
+         : kind == LK_UP2_F ? TileCfg{2, 2, 3, 32}                 // + 2-phase B tiles: 3 x 32-B chunks
          : (kind == LK_UP0_CONV2 || kind == LK_UP1_CONV2 || kind == LK_UP2_CONV2) ? TileCfg{4, 1, 3, 128}
                                                                                   : TileCfg{4, 1, 3, 64};
 }

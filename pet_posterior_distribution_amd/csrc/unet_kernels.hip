@@ -197,14 +197,17 @@ struct ConvGeom {
   static constexpr int CPR = ROWB / 16;             // 16-B pieces per LDS row
   static constexpr int KC = ROWB / (int)sizeof(T);  // input channels per chunk
   static constexpr int EPC = 16 / (int)sizeof(T);   // elements per 16-B piece
-  static constexpr int A_BYTES = ((AROWS + (FUSED ? 0 : 1)) * ROWB + 255) / 256 * 256;
+  // fused: A regions padded to whole wave instructions, so every wave issues the same DMA
+  // count (pieces past the rows land in the padding) and the counted ring waits stay uniform
+  static constexpr int APT_ = (AROWS * CPR + kThreads - 1) / kThreads;
+  static constexpr int A_BYTES = FUSED ? APT_ * kThreads * 16 : ((AROWS + 1) * ROWB + 255) / 256 * 256;
   static constexpr int B_BYTES = TAPS * NT * ROWB;
   // Fused up levels, segment 2 (coarse input b): A = S * L/2 rows, B = [phase][4 taps][NT][ROWB].
   // A stage holds either segment's layout; the zero row sits past both (ZOFF).
   static constexpr int LH = L / 2;
   static constexpr int AROWS2 = FUSED ? S * LH : 0;
   static constexpr int TAPS2 = 4;
-  static constexpr int A2_BYTES = (AROWS2 * ROWB + 255) / 256 * 256;
+  static constexpr int A2_BYTES = (AROWS2 * CPR + kThreads - 1) / kThreads * kThreads * 16;
   static constexpr int B2_BYTES = FUSED ? 2 * TAPS2 * NT * ROWB : 0;
   static constexpr int DATA = (A_BYTES + B_BYTES) > (A2_BYTES + B2_BYTES) ? A_BYTES + B_BYTES : A2_BYTES + B2_BYTES;
   static constexpr int ZOFF = FUSED ? DATA : ZROW * ROWB;    // byte offset of the zero row in a stage
@@ -212,12 +215,12 @@ struct ConvGeom {
   static constexpr int APIECES = AROWS * CPR;
   static constexpr int APT = (APIECES + kThreads - 1) / kThreads;
   static constexpr int BPT = B_BYTES / 16 / kThreads;
-  static constexpr bool AFULL = (APIECES % kThreads) == 0;
+  static constexpr bool AFULL = FUSED || (APIECES % kThreads) == 0;
   static constexpr int PER = APT + BPT;             // LDS-DMA instructions per wave per chunk
   static constexpr int APIECES2 = AROWS2 * CPR;
   static constexpr int APT2 = (APIECES2 + kThreads - 1) / kThreads;
   static constexpr int BPT2 = B2_BYTES / 16 / kThreads;
-  static constexpr bool AFULL2 = (APIECES2 % kThreads) == 0;
+  static constexpr bool AFULL2 = true;
   static constexpr int PER2 = APT2 + BPT2;          // segment-2 chunks
   static constexpr int PHROWS = FUSED ? S * LH : MT; // tile rows per output phase (fused)
   static constexpr int CT_LD = 2 * NT + 8;          // fp32 C tile, one ROW PAIR [c][2] per line (non-final)
@@ -249,7 +252,7 @@ struct ConvGeom {
   static_assert(WM * WN == 4, "4 waves");
   static_assert(MT % L == 0, "tile must hold whole samples");
   static_assert(B_BYTES % (16 * kThreads) == 0, "B tile split");
-  static_assert(ROWB == 64 || ROWB == 128, "row width");
+  static_assert(ROWB == 64 || ROWB == 128 || (ROWB == 32 && FUSED), "row width");
   static_assert(STAGES == 2 || (STAGES == 3 && AFULL && AFULL2), "3-stage ring needs uniform per-wave DMA counts");
   static_assert(PER < 64 && PER2 < 64, "vmcnt range");
   static_assert(!FUSED || (PHROWS % 96 == 0 && S % 2 == 0 && S <= 32 && B2_BYTES % (16 * kThreads) == 0),
@@ -259,7 +262,13 @@ struct ConvGeom {
   static_assert(EPI != EPI_FINAL || NT == 128, "final conv needs every channel in the tile");
   // XOR key of the 16-B piece index within a row: conflict-free ds_read_b128 for
   // 16 consecutive rows (lane groups of MI355X_MICROARCH.md LDS table)
-  static __device__ __forceinline__ int key(int row) { return CPR == 4 ? ((row >> 2) & 3) : ((row >> 1) & 7); }
+  static __device__ __forceinline__ int key(int row) {
+    return CPR == 4 ? ((row >> 2) & 3) : CPR == 2 ? ((row >> 3) & 1) : ((row >> 1) & 7);
+  }
+  // fused segment 1: LDS slot of input position p of sample s -- even positions first, then
+  // odd ones, sample-minor: the lanes of a fragment (one output phase, consecutive m or s)
+  // then read consecutive slots (conflict-free ds_read_b128 with key())
+  static __device__ __forceinline__ int slot1(int p, int s) { return ((p & 1) * (L / 2) + (p >> 1)) * S + s; }
   // tile row r -> (sample s, position l).  Fused tiles order their rows [phase e][m][sample]
   // (l = 2m + e), so every wave computes one output phase and the m = 0 rows (the only ones
   // whose composite taps need the left-edge correction) fill the first S rows of a phase.
@@ -326,7 +335,8 @@ struct DmaPlan {
       // LDS row: (sample, position) = row / LIN, row % LIN; fused: position-major slots
       // (row = li * S + s), so a lane group's 16 samples read 16 consecutive rows
       const int s = G::FUSED ? row % G::S : row / G::LIN;
-      const int li = G::FUSED ? row / G::S : row - s * G::LIN;
+      const int q1 = row / G::S;                 // fused: slot1 position index
+      const int li = G::FUSED ? (q1 < G::LH ? 2 * q1 : 2 * (q1 - G::LH) + 1) : row - s * G::LIN;
       const int b = min(m0 + s, a.B - 1);        // rows of absent samples only feed unstored outputs
       avoff1[qq] = ((b * G::LIN + li) * a.c1 + c * G::EPC) * (int)sizeof(T);
       avoff2[qq] = ((b * G::LIN + li) * a.c2 + c * G::EPC) * (int)sizeof(T);
@@ -592,7 +602,7 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
       G::row_sl(r, s, l);
       const int p = l + j - PADL;
       int row;
-      if (G::FUSED) row = (p >= 0 && p < L) ? p * G::S + s : G::ZROW;
+      if (G::FUSED) row = (p >= 0 && p < L) ? G::slot1(p, s) : G::ZROW;
       else if (!UPS) row = (p >= 0 && p < L) ? s * L + p : G::ZROW;
       else row = (p < L) ? s * G::LIN + (p >> 1) : G::ZROW;
       aoff[j][i] = (G::FUSED && row == G::ZROW) ? G::ZOFF + (c0 << 4) : row * ROWB + ((c0 ^ G::key(row)) << 4);
