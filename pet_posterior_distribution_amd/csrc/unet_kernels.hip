@@ -241,7 +241,15 @@ struct ConvGeom {
   static constexpr int TAIL = PREMAP ? TAC_OFF + (S + 1) * 4 : 0;
   static_assert(S <= 64, "one wave gathers the block's condition indices");
   static constexpr int SMEM0 = EPI_BYTES > RING ? EPI_BYTES : RING;
-  static constexpr int SMEM = SMEM0 > TAIL ? SMEM0 : TAIL;
+  // fused final level: its time and label map rows [L][FIN_LD] fp32 (padded rows: the row loop's
+  // lanes read consecutive rows conflict-free) prefetched behind the ring at kernel start
+  static constexpr bool FIN_MAPS = FUSED && EPI == EPI_FINAL;
+  static constexpr int FMAP_PIECES = L * (FIN_LD / 4);                 // per map, incl. one pad piece per row
+  static constexpr int FMAP_OFF = (SMEM0 + 15) / 16 * 16;
+  static constexpr int FMAP_BYTES = FIN_MAPS ? 2 * FMAP_PIECES * 16 : 0;
+  static constexpr int SMEM1 = SMEM0 > TAIL ? SMEM0 : TAIL;
+  static constexpr int SMEM = FIN_MAPS ? FMAP_OFF + FMAP_BYTES : SMEM1;
+  static_assert(!FIN_MAPS || (TAIL == 0 && FIN_LD == 132 && NT == 128), "final map layout");
   static_assert(!PREMAP || EPI_BYTES <= RING, "C tile must not overlap the prefetched maps");
   // Dedicated loader waves (16-bit 3-stage layers): 4 extra waves issue every LDS-DMA
   // piece, so the 4 MFMA waves never stall on DMA issue.
@@ -887,6 +895,34 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
 #endif
   using Seg1 = std::integral_constant<int, 1>;
   using Seg2 = std::integral_constant<int, 2>;
+  // fused final level, t uniform and one condition in the tile: map rows into LDS (FMAP_OFF)
+  bool fin_fast = false;
+  auto prefetch_fin_maps = [&]() {
+    if constexpr (G::FIN_MAPS) {
+      const int tac0f = a.tac ? a.tac[min(m0, B - 1)] : 0;
+      fin_fast = a.t_uniform >= 0 && a.tmap && a.cmap;
+      if (a.tac)
+        for (int k = 1; k < G::S; ++k) fin_fast = fin_fast && (m0 + k >= B || a.tac[m0 + k] == tac0f);
+      if (!fin_fast) return;
+      const i32x4 rs_t = make_rsrc(a.tmap, (unsigned)a.n_t * L * (unsigned)a.cout * 4u);
+      const i32x4 rs_c = make_rsrc(a.cmap, (unsigned)a.n_tac * L * (unsigned)a.cout * 4u);
+      constexpr int NPI = (G::FMAP_PIECES + kThreads - 1) / kThreads;
+#pragma unroll
+      for (int mp = 0; mp < 2; ++mp)
+#pragma unroll
+        for (int k = 0; k < NPI; ++k) {
+          const int p0 = k * kThreads + wv * 64, q = p0 + lane;
+          if (q < G::FMAP_PIECES) {
+            const int l = q / (G::FIN_LD / 4), c = min(q - l * (G::FIN_LD / 4), NT / 4 - 1);   // pad piece: a copy
+            const int row = mp ? tac0f : a.t_uniform;
+            llvm_amdgcn_raw_buffer_load_lds(mp ? rs_c : rs_t,
+                                            (__attribute__((address_space(3))) void*)(smem + G::FMAP_OFF +
+                                                                                        (mp * G::FMAP_PIECES + p0) * 16),
+                                            16, ((row * L + l) * a.cout + c * 4) * 4, 0, 0, 0);
+          }
+        }
+    }
+  };
   using Seg2Next = std::integral_constant<int, 3>;
   if constexpr (G::FUSED) {
     // Fused up level: segment-1 chunks (skip s), then segment-2 chunks (coarse b); every
@@ -918,6 +954,7 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
     } else {
       dma.all(smem, 0, 0, lane);
       prefetch_maps();
+      prefetch_fin_maps();
       ring_barrier<0>();
       compute(smem, Two{}, 1, 1, Seg1{}, 0);              // chunks 1, 2 -> stages 1, 2
       ring_barrier<G::PER>();
@@ -1225,20 +1262,28 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
       const float* mp = a.tmap ? a.tmap + ((size_t)t * L + l) * cout : nullptr;
       const float* cp = a.cmap ? a.cmap + ((size_t)tac * L + l) * cout : nullptr;
       f32x4 o4 = {0.f, 0.f, 0.f, 0.f};
+      auto dot = [&](const float* mq, const float* cq) {
 #pragma unroll 4
-      for (int n = 0; n < 128; n += 4) {
-        f32x4 hv = *reinterpret_cast<const f32x4*>(fin + r * G::FIN_LD + n);
-        hv += mp ? *reinterpret_cast<const f32x4*>(mp + n) : *reinterpret_cast<const f32x4*>(a.bias + n);
-        if (cp) hv += *reinterpret_cast<const f32x4*>(cp + n);
+        for (int n = 0; n < 128; n += 4) {
+          f32x4 hv = *reinterpret_cast<const f32x4*>(fin + r * G::FIN_LD + n);
+          hv += mq ? *reinterpret_cast<const f32x4*>(mq + n) : *reinterpret_cast<const f32x4*>(a.bias + n);
+          if (cq) hv += *reinterpret_cast<const f32x4*>(cq + n);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float hq = fmaxf(hv[q], 0.f);
-          const f32x4 wq = *reinterpret_cast<const f32x4*>(wfl + (n + q) * 4);
-          o4[0] = fmaf(hq, wq[0], o4[0]);
-          o4[1] = fmaf(hq, wq[1], o4[1]);
-          o4[2] = fmaf(hq, wq[2], o4[2]);
-          o4[3] = fmaf(hq, wq[3], o4[3]);
+          for (int q = 0; q < 4; ++q) {
+            const float hq = fmaxf(hv[q], 0.f);
+            const f32x4 wq = *reinterpret_cast<const f32x4*>(wfl + (n + q) * 4);
+            o4[0] = fmaf(hq, wq[0], o4[0]);
+            o4[1] = fmaf(hq, wq[1], o4[1]);
+            o4[2] = fmaf(hq, wq[2], o4[2]);
+            o4[3] = fmaf(hq, wq[3], o4[3]);
+          }
         }
+      };
+      if (G::FIN_MAPS && fin_fast) {                 // the same map rows, prefetched into LDS
+        const float* lm = reinterpret_cast<const float*>(smem + G::FMAP_OFF) + l * G::FIN_LD;
+        dot(lm, lm + G::FMAP_PIECES * 4);
+      } else {
+        dot(mp, cp);
       }
       float o[4];
 #pragma unroll
