@@ -576,7 +576,9 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
   const int bid = blockIdx.x;
   const int xcd = bid & 7, loc = bid >> 3, q8 = total >> 3, r8 = total & 7;
 #ifndef CONV_XCD_MAP
-#define CONV_XCD_MAP 1    // 0: identity, 1: XCD-contiguous slots N-fastest, 2: XCD-contiguous slots M-fastest
+#define CONV_XCD_MAP 1    // 0: identity, 1: XCD-contiguous slots N-fastest, 2: XCD-contiguous slots M-fastest,
+                          // 3: a (bm x 4) block of the tile grid per XCD when the grid splits evenly, else 1
+                          //    (A/B: 4257/4266 vs 4295/4303 samples/s for 1, so 1 stays)
 #endif
 #if CONV_XCD_MAP == 0
   const int slot = bid;
@@ -585,6 +587,15 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
 #endif
 #if CONV_XCD_MAP == 2
   const int n_tile = slot / nM, m_tile = slot - n_tile * nM;
+#elif CONV_XCD_MAP == 3
+  // per XCD: bn = min(nN, 4) N tiles x bm = total / 8 / bn M tiles, so its L2 holds a few
+  // M tiles' activations and a few N tiles' weights (down3, up0: 8 x 4 instead of 2 x 16 /
+  // 4 x 8, about 20-30% less weight traffic through the XCD's L2)
+  const int bn = nN < 4 ? nN : 4, per = total >> 3, bm = per / bn;
+  const bool blk = r8 == 0 && per % bn == 0 && nN % bn == 0 && nM % bm == 0;
+  const int ncb = nN / bn;
+  const int m_tile = blk ? (xcd / ncb) * bm + loc / bn : slot / nN;
+  const int n_tile = blk ? (xcd % ncb) * bn + loc % bn : slot - (slot / nN) * nN;
 #else
   const int m_tile = slot / nN, n_tile = slot - m_tile * nN;
 #endif
