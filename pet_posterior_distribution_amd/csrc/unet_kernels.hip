@@ -93,6 +93,16 @@ __device__ __forceinline__ void philox_normal2(unsigned long long seed, unsigned
                                                float* z) {
   uint32_t c[4] = {(uint32_t)roi, (uint32_t)step, (uint32_t)(g & 0xffffffffull), (uint32_t)(g >> 32)};
   philox4x32_10(c, (uint32_t)(seed & 0xffffffffull), (uint32_t)(seed >> 32));
+#if FIN_EXP & 8   // diagnostic timing build: fp32 Box-Muller
+  {
+    const float r = sqrtf(2.0f * (22.18070977791825f - logf((float)c[0] + 1.0f)));
+    float sn, cs;
+    sincosf(6.283185307179586f * (((float)c[1] + 0.5f) * 2.3283064365386963e-10f), &sn, &cs);
+    z[0] = r * cs;
+    z[1] = r * sn;
+    return;
+  }
+#endif
   const double u1 = ((double)c[0] + 1.0) * 2.3283064365386963e-10;
   const double u2 = ((double)c[1] + 0.5) * 2.3283064365386963e-10;
   const double r = sqrt(-2.0 * log(u1));
