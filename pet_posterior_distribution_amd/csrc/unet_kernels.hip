@@ -34,6 +34,12 @@
 #ifndef CONV_EXP_MODE
 #define CONV_EXP_MODE 0
 #endif
+// Diagnostic builds only: final-level epilogue parts dropped for timing (1: the fused next-step
+// down0, 2: its s0 / p0 stores, 4: the final-conv / p_sample row loop, 8: fp32 Box-Muller).
+// The product is built with 0.
+#ifndef FIN_EXP
+#define FIN_EXP 0
+#endif
 
 namespace petdiff {
 
@@ -531,12 +537,14 @@ __device__ __forceinline__ void down0_positions(const Down0Args& a, const float*
         v[e][q] = fmaxf(acc0[q] + m0[q], 0.f);
         v[e][4 + q] = fmaxf(acc1[q] + m1[q], 0.f);
       }
-      Vec8<T>::store(reinterpret_cast<T*>(a.s0) + ((size_t)b * 48 + l) * 128 + n0, v[e]);
+      if constexpr (!(FIN_EXP & 2)) Vec8<T>::store(reinterpret_cast<T*>(a.s0) + ((size_t)b * 48 + l) * 128 + n0, v[e]);
+      else if (v[e][0] == 12345.f) reinterpret_cast<T*>(a.s0)[0] = (T)0.f;
     }
     float pv[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) pv[q] = fmaxf(v[0][q], v[1][q]);
-    Vec8<T>::store(reinterpret_cast<T*>(a.p0) + ((size_t)b * 24 + lp) * 128 + n0, pv);
+    if constexpr (!(FIN_EXP & 2)) Vec8<T>::store(reinterpret_cast<T*>(a.p0) + ((size_t)b * 24 + lp) * 128 + n0, pv);
+    else if (pv[0] == 12345.f) reinterpret_cast<T*>(a.p0)[0] = (T)0.f;
   }
 }
 
@@ -1278,6 +1286,7 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
     for (int r = tid; r < G::MT; r += kThreads) {
       const int s = r / L, l = r - s * L, b = m0 + s;
       if (b >= B) continue;
+      if constexpr ((FIN_EXP & 4) != 0) { xst[r * 2] = xst[r * 2 + 1] = fin[r * G::FIN_LD]; continue; }
       const int tac = a.tac ? a.tac[b] : 0;
       const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[b];
       const float* mp = a.tmap ? a.tmap + ((size_t)t * L + l) * cout : nullptr;
@@ -1351,7 +1360,7 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
         for (int k = 0; k < 6; ++k) reinterpret_cast<f32x4*>(mp)[tid + kThreads * k] = mv[k];
       }
       __syncthreads();
-      down0_positions<T>(nd, xst, mp, fast, m0, nb_next, wr, n0_next, tid >> 4, kThreads / 16);
+      if constexpr (!(FIN_EXP & 1)) down0_positions<T>(nd, xst, mp, fast, m0, nb_next, wr, n0_next, tid >> 4, kThreads / 16);
     }
   }
 }
