@@ -374,3 +374,29 @@ def test_fused_up_loop_vs_unfused(conds, monkeypatch):
     assert np.abs(a.std(0) - b.std(0)).max() < 0.1 * b.std(0).mean()
     plain.close()
     fused.close()
+
+
+@pytest.mark.parametrize('lv,param', [('learn_ranged', 'eps'), ('', 'eps'), ('learn_ranged', 'v')])
+def test_p_sample_bf16_fused_levels(conds, lv, param):
+    """p_sample through the 16-bit network (fused up levels; the final conv + p_sample epilogue
+    writing mean / var / var_tilde).  The bf16 network output is checked against the fp64 oracle
+    network (3e-2), and the fp32 p_sample epilogue against the oracle's p_mean_variance applied
+    to that same network output (1e-4); t = 0 exactly noise-free; per-sample conditions and t."""
+    m = make_model('bfloat16', seed=6, learn_variance=lv, parameterization=param, final_scale=0.2)
+    rng = np.random.default_rng(26)
+    B = 9
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    t = np.array([999, 800, 600, 400, 100, 10, 2, 1, 0], dtype=np.int32)
+    z = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    table = np.stack([conds[0], conds[1]])
+    cond = table[rng.integers(0, 2, B)]
+    net = m.call({'x': x, 'time': t, 'condition': cond}).cpu().numpy().astype(np.float64)
+    assert rel(net, R.unet_forward(m.network.weights, x, t, cond, dt=np.float64)) < 3e-2
+    mean, var, var_t = m.ddpm(x, t, cond, z=z)
+    out = R.p_mean_variance(S, net, x.astype(np.float64), t, lv, param, dt=np.float64)
+    mask = np.where(t == 0, 0., 1.).reshape(-1, 1, 1)
+    assert rel(mean, out['mean']) < 1e-4
+    assert rel(var, mask * np.exp(0.5 * out['log_variance']) * z) < 1e-4
+    assert rel(var_t, mask * np.exp(0.5 * out['log_variance_tilde']) * z) < 1e-4
+    assert float(var[-1].abs().max()) == 0.0
+    m.close()
