@@ -63,6 +63,47 @@ def parse():
     return ap.parse_args()
 
 
+def init_dist():
+    """One process per GPU (torch.distributed.run env).  Returns (world, rank, device).
+
+    The collective backend is RCCL ('nccl').  PETDIFF_BENCH_BACKEND=gloo is a rehearsal mode for a
+    box with fewer GPUs than ranks: ranks share devices round-robin (LOCAL_RANK mod device count)
+    and the few small collectives (barrier, max of the timer, stats all-gather) go over gloo on host
+    tensors.  RCCL refuses two ranks on one GPU, so this is how the N>1 code path of this file is
+    exercised on a 1-GPU box; the timed region is the same either way."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        os.environ.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+        backend = os.environ.get('PETDIFF_BENCH_BACKEND', 'nccl')
+        if backend == 'gloo':
+            torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
+            dist.init_process_group('gloo')
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, torch.device('cuda', torch.cuda.current_device())
+
+
+def coll_device(dev):
+    """Where collective operands live: the GPU for RCCL, the host for the gloo rehearsal."""
+    import torch.distributed as dist
+    return 'cpu' if dist.get_backend() == 'gloo' else dev
+
+
+def max_over_ranks(elapsed, dev):
+    import torch
+    import torch.distributed as dist
+    e = torch.tensor([elapsed], device=coll_device(dev), dtype=torch.float64)
+    dist.all_reduce(e, op=dist.ReduceOp.MAX)
+    return float(e.item())
+
+
 def host_threads():
     """CPU threads for the baseline leg: the job's CPU share (OMP_NUM_THREADS on the GPU
     box, 16 per GPU), never the whole machine's core count."""
@@ -148,14 +189,7 @@ def main_mh(args):
     (weak scaling over ranks: every rank runs its own chains of its own TAC)."""
     import torch
     import torch.distributed as dist
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    else:
-        torch.cuda.set_device(0)
+    world, rank, dev = init_dist()
     from pet_posterior_distribution_amd.mcmc import MetropolisSRTM2
     from pet_posterior_distribution_amd.sim_data import mh_problem
     P = mh_problem(seed=rank)
@@ -172,9 +206,7 @@ def main_mh(args):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        e = torch.tensor([elapsed], device='cuda', dtype=torch.float64)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+        elapsed = max_over_ranks(elapsed, dev)
     # the reference's protocol per TAC (main_script.py:363-364; pymc default 4 chains):
     # 4 chains x (20k draws + 40k tune), timed on a 1/50 slice and scaled
     t1 = time.perf_counter()
@@ -231,16 +263,7 @@ def main_train(args):
     tests/test_cpu_train.py gloo test); training data = the GPU synthetic-TAC generator (row 3)."""
     import torch
     import torch.distributed as dist
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        os.environ.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device('cuda', torch.cuda.current_device())
+    world, rank, dev = init_dist()
     from pet_posterior_distribution_amd import ImprovedDDPM, UnetConditional, Adam, ExponentialDecay
     from pet_posterior_distribution_amd.configs import shipped_net_args, shipped_diff_args
     from pet_posterior_distribution_amd.networks import glorot_uniform_init
@@ -268,7 +291,12 @@ def main_train(args):
                              sample_offset=rank * B, loss=loss)
         if world > 1:
             g = tr.gradients()
-            dist.all_reduce(g)
+            if coll_device(dev) == 'cpu':
+                gh = g.cpu()
+                dist.all_reduce(gh)
+                g.copy_(gh)
+            else:
+                dist.all_reduce(g)
             tr.set_gradients(g)
         tr.apply_gradients(1.0)
 
@@ -287,9 +315,7 @@ def main_train(args):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+        elapsed = max_over_ranks(elapsed, dev)
     stats = tr.last_stats()
     if rank == 0:
         samples = world * B * args.steps
@@ -326,16 +352,7 @@ def main():
         return main_train(args)
     import torch
     import torch.distributed as dist
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        os.environ.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device('cuda', torch.cuda.current_device())
+    world, rank, dev = init_dist()
 
     from pet_posterior_distribution_amd import ImprovedDDPM, UnetConditional
     from pet_posterior_distribution_amd.sim_data import make_condition
@@ -376,13 +393,11 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+        elapsed = max_over_ranks(elapsed, dev)
 
     # posterior summary: per-rank Welford partials, RCCL all-gather
     st = model.posterior_stats(out, tac=tac if n_tac > 1 else None, n_tac=n_tac)   # (n_tac, 48, 2, 3) fp64
-    st_t = torch.as_tensor(st, device=dev)
+    st_t = torch.as_tensor(st, device=coll_device(dev) if world > 1 else dev)
     ag_ms = 0.0
     if world > 1:
         gathered = [torch.empty_like(st_t) for _ in range(world)]

@@ -55,6 +55,14 @@ extern "C" {
 #define PETDIFF_ERR_HIP 2          /* HIP runtime failure (RuntimeError)      */
 #define PETDIFF_ERR_UNSUPPORTED 3  /* config outside the compiled kernels     */
 
+/* Largest batch one call accepts (posterior samples per launch).  Every activation
+ * buffer then stays below 2^31 elements and 4 GB, which the kernels' 32-bit row
+ * indices and buffer-resource record counts assume.  ImprovedDDPM.ddpm_loop splits
+ * larger batches into chunks (the noise stream is keyed by global sample index, so
+ * chunked and unchunked runs are identical), as main_script.py:414-427 chunks its
+ * own posterior draws. */
+#define PETDIFF_MAX_BATCH 65536
+
 #define PETDIFF_DTYPE_F32 0        /* exact-f32 MFMA network (parity mode)    */
 #define PETDIFF_DTYPE_BF16 1       /* bf16 MFMA network, fp32 accumulate + fp32 p_sample */
 #define PETDIFF_DTYPE_F16 2        /* fp16 MFMA network (BASELINE config 5), fp32 accumulate + p_sample */

@@ -19,6 +19,7 @@ DTYPE_F32, DTYPE_BF16, DTYPE_F16 = 0, 1, 2
 LEARN_FIXED, LEARN, LEARN_RANGED = 0, 1, 2
 PARAM_EPS, PARAM_X0, PARAM_V, PARAM_XPREV = 0, 1, 2, 3
 NTAB = 13
+MAX_BATCH = 65536                    # PETDIFF_MAX_BATCH (include/petdiff.h)
 NUM_LAYERS = 10
 LAYER_NAMES = ['down0', 'down1', 'down2', 'down3', 'up0.conv2', 'up0.block', 'up1.conv2',
                'up1.block', 'up2.conv2', 'up2.block+final+p_sample']

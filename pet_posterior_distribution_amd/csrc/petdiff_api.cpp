@@ -311,6 +311,7 @@ int fused_maps(petdiff_ctx* h, int u, bool time, int n, hipStream_t s) {
 }
 
 int ensure_workspace(petdiff_ctx* h, int B) {
+  if (B > PETDIFF_MAX_BATCH) return fail(PETDIFF_ERR_INVALID, "batch exceeds PETDIFF_MAX_BATCH (65536); split it into chunks");
   if (B <= h->B_cap) return PETDIFF_OK;
   const size_t e = h->act_bytes();
   const size_t Bz = (size_t)B;

@@ -430,10 +430,25 @@ class ImprovedDDPM:
         if seed is None:
             seed = self.seed + self._call_counter
             self._call_counter += 1
-        _lib.check(_lib.lib().petdiff_generate(
-            self._handle, _ptr(x), _ptr(tac), tseq.ctypes.data_as(C.c_void_p), n, int(bool(flag_var_tilde)),
-            _ptr(zt), int(seed), int(sample_offset), _ptr(out), _ptr(all_xt), B, int(bool(use_graph)),
-            _stream_ptr(self.device)), 'petdiff_generate')
+        # batches above PETDIFF_MAX_BATCH run as chunks (main_script.py:414-427 chunks the same way);
+        # sample b of chunk c is global sample sample_offset + c0 + b, so the noise is unchanged
+        for c0 in range(0, B, _lib.MAX_BATCH):
+            c1 = min(B, c0 + _lib.MAX_BATCH)
+            whole = c0 == 0 and c1 == B
+            xc = x if whole else x[c0:c1].contiguous()
+            tc = tac if (whole or tac is None) else tac[c0:c1].contiguous()
+            zc = zt if (whole or zt is None) else zt[:, c0:c1].contiguous()
+            oc = out if whole else torch.empty_like(xc)
+            ac = all_xt if (whole or all_xt is None) else torch.empty((n,) + tuple(xc.shape), dtype=torch.float32,
+                                                                      device=self.device)
+            _lib.check(_lib.lib().petdiff_generate(
+                self._handle, _ptr(xc), _ptr(tc), tseq.ctypes.data_as(C.c_void_p), n, int(bool(flag_var_tilde)),
+                _ptr(zc), int(seed), int(sample_offset) + c0, _ptr(oc), _ptr(ac), c1 - c0, int(bool(use_graph)),
+                _stream_ptr(self.device)), 'petdiff_generate')
+            if not whole:
+                out[c0:c1] = oc
+                if all_xt is not None:
+                    all_xt[:, c0:c1] = ac
         if keep_all_xt:
             return all_xt.cpu().numpy()
         return out

@@ -208,6 +208,32 @@ def test_graph_equals_eager_and_shard_invariance(m16, conds):
     torch.testing.assert_close(a, torch.cat([c1, c2]), rtol=0, atol=0)
 
 
+def test_chunked_generate_bitwise(m16, conds, monkeypatch):
+    """Batches above PETDIFF_MAX_BATCH run as chunks with advancing sample offsets: bitwise equal to
+    one launch (chunk size lowered here so the test stays small), for keep_all_xt and per-sample tac."""
+    from pet_posterior_distribution_amd import _lib
+    rng = np.random.default_rng(19)
+    B = 100
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    tac = (np.arange(B) % 2).astype(np.int32)
+    a = m16.ddpm_loop(x, conds, num_timesteps=20, seed=7, tac=tac)
+    ka = m16.ddpm_loop(x, conds[:1], num_timesteps=5, seed=8, keep_all_xt=True)
+    monkeypatch.setattr(_lib, 'MAX_BATCH', 40)
+    b = m16.ddpm_loop(x, conds, num_timesteps=20, seed=7, tac=tac)
+    kb = m16.ddpm_loop(x, conds[:1], num_timesteps=5, seed=8, keep_all_xt=True)
+    torch.testing.assert_close(a, b, rtol=0, atol=0)
+    np.testing.assert_array_equal(ka, kb)
+
+
+def test_batch_above_max_rejected(m16, conds):
+    """The C ABI refuses one launch above PETDIFF_MAX_BATCH (ValueError in the wrapper), before
+    allocating or launching anything."""
+    from pet_posterior_distribution_amd import _lib
+    x = torch.zeros((_lib.MAX_BATCH + 1, 48, 2), device='cuda')
+    with pytest.raises(ValueError, match='PETDIFF_MAX_BATCH'):
+        m16.ddpm(x, np.zeros(_lib.MAX_BATCH + 1, np.int32), conds[:1])
+
+
 def test_bf16_loop_statistics_vs_f32(m16, m32, conds):
     """bf16 network vs exact-f32 network on the same noise: posterior moments agree statistically."""
     rng = np.random.default_rng(10)
