@@ -6,6 +6,7 @@ along random directions of individual parameter tensors; the loss terms and the
 optimizer against closed forms.
 """
 import math
+import zlib
 
 import numpy as np
 import pytest
@@ -48,18 +49,25 @@ def test_gradient_vs_finite_differences(setup, name):
     P, x0, cond, t, noise, loss, mse, vlb, G = setup
     xt = S['sqrt_alpha_bar'][t].reshape(-1, 1, 1) * x0 + S['sqrt_one_minus_alpha_bar'][t].reshape(-1, 1, 1) * noise
     pred = R.unet_forward(P, xt, t, cond, dt=np.float64)[..., :2]
-    rng = np.random.default_rng(abs(hash(name)) % 2 ** 32)
-    D = rng.standard_normal(P[name].shape)
-    eps = 1e-6 * max(1.0, float(np.abs(P[name]).max())) / max(1.0, float(np.abs(D).max()))
+    # The objective is piecewise smooth (ReLU, max-pool): a direction whose +-eps segment crosses a
+    # kink gives a wrong central difference (eps 1e-8 keeps that rare even for the 3M-entry up0 kernel,
+    # about 18k ReLU units).  Three fixed directions (str hash() is salted per
+    # process, so seeds come from crc32); at least two must agree to 1e-5.
+    res = []
+    for k in range(3):
+        rng = np.random.default_rng(zlib.crc32(name.encode()) + k)
+        D = rng.standard_normal(P[name].shape)
+        eps = 1e-8 * max(1.0, float(np.abs(P[name]).max())) / max(1.0, float(np.abs(D).max()))
 
-    def J(s):
-        Q = dict(P)
-        Q[name] = P[name] + s * D
-        return TR.objective(Q, S, x0, cond, t, noise, pred)
+        def J(s):
+            Q = dict(P)
+            Q[name] = P[name] + s * D
+            return TR.objective(Q, S, x0, cond, t, noise, pred)
 
-    fd = (J(eps) - J(-eps)) / (2 * eps)
-    an = float((G[name] * D).sum())
-    assert abs(fd - an) <= 1e-5 * max(abs(an), 1e-3), (name, fd, an)
+        fd = (J(eps) - J(-eps)) / (2 * eps)
+        an = float((G[name] * D).sum())
+        res.append((abs(fd - an) <= 1e-5 * max(abs(an), 1e-3), fd, an))
+    assert sum(r[0] for r in res) >= 2, (name, res)
 
 
 def test_decoder_nll_gradient_finite_differences():
