@@ -50,6 +50,10 @@ def parse():
     ap.add_argument('--batch', type=int, default=1024, help='posterior samples per GPU')
     ap.add_argument('--tacs', type=int, default=1,
                     help='test TACs per GPU (samples split TAC-major; config 4 = 32 TACs x 8192 per GPU)')
+    ap.add_argument('--chunk', type=int, default=0,
+                    help='samples per launch (0 = PETDIFF_MAX_BATCH); larger batches run as chunks')
+    ap.add_argument('--config4', action='store_true',
+                    help='BASELINE configs[3] per-rank shard: 32 TACs x 8192 posterior samples per GPU')
     ap.add_argument('--reverse-steps', type=int, default=1000)
     ap.add_argument('--dtype', default='bfloat16', choices=['bfloat16', 'float16', 'float32'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -361,6 +365,14 @@ def main():
     net = UnetConditional(**shipped_net_args(), seed=1234)
     net.build((None, 48, 2))
     model = ImprovedDDPM(network=net, dtype=args.dtype, device=dev.index, **shipped_diff_args())
+    if args.config4:
+        args.batch, args.tacs = 32 * 8192, 32
+    from pet_posterior_distribution_amd import _lib
+    if args.chunk:
+        if not 0 < args.chunk <= _lib.MAX_BATCH:
+            raise SystemExit(f'--chunk must be in [1, {_lib.MAX_BATCH}]')
+        _lib.MAX_BATCH = args.chunk
+    chunk = _lib.MAX_BATCH
     B = args.batch
     n_tac = args.tacs
     if n_tac < 1 or B % n_tac:
@@ -415,8 +427,9 @@ def main():
     layer_ms = None
     if not args.no_kernel_timing:
         model.set_kernel_timing(True)
-        model.ddpm_loop(x_T, cond, num_timesteps=n_rev, seed=2, sample_offset=offset, use_graph=False,
-                        tac=tac if n_tac > 1 else None)
+        bt = min(B, chunk)   # one launch's worth of samples
+        model.ddpm_loop(x_T[:bt], cond, num_timesteps=n_rev, seed=2, sample_offset=offset, use_graph=False,
+                        tac=tac[:bt] if n_tac > 1 else None)
         layer_ms = model.get_kernel_timing()
         model.set_kernel_timing(False)
 
@@ -432,13 +445,13 @@ def main():
             fused_up = layer_ms['up0.conv2'][1] == 0      # the k2 conv runs inside the block kernel
             alg = UP0_BLOCK_FLOP_PER_SAMPLE + (UP0_CONV2_FLOP_PER_SAMPLE if fused_up else 0)
             exe = UP0_FUSED_EXEC_FLOP_PER_SAMPLE if fused_up else UP0_BLOCK_EXEC_FLOP_PER_SAMPLE
-            ach = alg * B / avg_s / 1e12
+            ach = alg * bt / avg_s / 1e12
             kname = ('conv_kernel<up0 fused> (UpSampling1D + k2 conv 1074->512 + ConvBlock 1024->512 k6+res, L=12)'
                      if fused_up else 'conv_kernel<up0.block> (L=12, 1024->512, k6+res)')
             roof = {'bound': 'mfma', 'kernel': kname,
                     'achieved': round(ach, 2), 'peak': peak, 'unit': 'TFLOP/s', 'frac': round(ach / peak, 4),
-                    'traffic': load_traffic(fused_up), 'avg_launch_us': round(avg_s * 1e6, 2),
-                    'executed_tflops': round(exe * B / avg_s / 1e12, 2),
+                    'traffic': load_traffic(fused_up) if bt == 1024 else None, 'avg_launch_us': round(avg_s * 1e6, 2),
+                    'executed_tflops': round(exe * bt / avg_s / 1e12, 2),
                     'pipeline_tflops': round(tflops_pipeline, 2),
                     'pipeline_frac': round(tflops_pipeline / peak, 4)}
         line = {
@@ -449,7 +462,8 @@ def main():
             'data': 'synthetic (SRTM2 TACs + noise model; identity-denoiser Glorot weights of the shipped net)',
             'config': {'workload': 'iDDPM reverse process, f128/d4 1-D conditional U-Net, 48-ROI x 2 params',
                        'n_posterior_per_gpu': B, 'reverse_steps': n_rev, 'global_batch': world * B,
-                       'tacs': world * n_tac, 'parallelism': f'dp{world} (sample shards, RCCL all-gather of stats)',
+                       'tacs': world * n_tac, 'samples_per_launch': min(B, chunk),
+                       'parallelism': f'dp{world} (sample shards, RCCL all-gather of stats)',
                        'hipgraph': True},
             'roofline': roof,
             'outputs_finite': finite,

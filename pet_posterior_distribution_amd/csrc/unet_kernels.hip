@@ -40,6 +40,13 @@
 #ifndef FIN_EXP
 #define FIN_EXP 0
 #endif
+// Tap reuse in registers (fused levels whose fragments each hold ONE position of 32 samples,
+// i.e. up0): a wave's 3 fragments sit at positions 2 (segment 1) or 1 (segment 2) apart, so the
+// taps' A fragments are 10 (resp. 6) distinct LDS rows instead of 18 (12).  0 = one read per
+// (tap, fragment) as in the other layers (A/B switch).
+#ifndef CONV_TAP_REUSE
+#define CONV_TAP_REUSE 1
+#endif
 
 namespace petdiff {
 
@@ -715,6 +722,14 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
       bv[0][1][e] = bv[1][0][e] = (decltype(bv[0][0][0]))(0.02f * (lane - e));
     }
   }
+  // Tap reuse (CONV_TAP_REUSE): this wave's fragment i at tap j reads fine position P = 2i + j
+  // (segment 1) or coarse row Q = i + k (segment 2) relative to its first fragment; each step
+  // reads only the positions no earlier step of its k-group has read.  cav carries the last
+  // step's A operands into the next chunk's first step (whose MFMAs they are).
+  constexpr bool REUSE = CONV_TAP_REUSE && G::FUSED && G::S == 32 && sizeof(T) == 2;
+  fragT cav[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) cav[i] = fragT{};
   auto mfma_bf16 = [&](int pb) {
 #pragma unroll
     for (int i = 0; i < 3; ++i)
@@ -749,7 +764,121 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
     constexpr int NEXT = (int)decltype(next_tag)::value;
     constexpr int SEG = (int)decltype(seg_tag)::value;
     char* nbase = smem + nbuf * G::STAGE;
-    if constexpr (sizeof(T) == 2) {
+    if constexpr (REUSE) {
+      constexpr int NG = ROWB / 32;
+      constexpr int NT_ = SEG == 2 ? G::TAPS2 : TAPS;
+      constexpr int NS = NT_ * NG;
+      constexpr int D = SEG == 2 ? 1 : 2;                 // position step between fragments
+      constexpr int NPOS = NT_ + 2 * D;
+      constexpr int NPER = NEXT == 3 ? G::PER2 : G::PER;
+      constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;
+      constexpr int PPS = (NPC + NS - 1) / NS;
+      static_assert(NS % 2 == 0, "B double buffer alternates per step");
+      fragT AP[NG][NPOS];
+      fragT am[SEG == 2 ? NG : 1];
+      // LDS offset of relative position P (any (tap, fragment) pair that lands on it)
+      auto posoff = [&](int P) -> int {
+        if constexpr (SEG == 2) {
+          const int i = P < 2 ? P : 2;
+          return aoff2[P - i][i];
+        } else {
+          const int i = P / 2 < 2 ? P / 2 : 2;
+          return aoff[P - 2 * i][i];
+        }
+      };
+      // segment-1 tap order 0 2 4 1 3 5: consecutive taps of one parity share 2 of 3 positions
+      auto tap_of = [](int jj) { return SEG == 2 ? jj : (jj < 3 ? 2 * jj : 2 * (jj - 3) + 1); };
+#pragma unroll
+      for (int st = 0; st < NS; ++st) {
+        const int g = st / NT_, jj = st % NT_, sb = st & 1, pb = sb ^ 1;
+        const int j = tap_of(jj);
+        const bool full = SEG == 2 ? jj == 0 : (jj == 0 || jj == 3);
+        const int sp = st == 0 ? 0 : st - 1;
+        const int gp = sp / NT_, jp = tap_of(sp % NT_);
+        const char* pb0 = base + ((boff[0] + j * NT * ROWB) ^ (g << 5));
+        const char* pb1 = base + ((boff[1] + j * NT * ROWB) ^ (g << 5));
+        if constexpr (SEG == 2) {
+          pb0 = base + ((boff2[0] + j * NT * ROWB) ^ (g << 5));
+          pb1 = base + ((boff2[1] + j * NT * ROWB) ^ (g << 5));
+        }
+#define PETDIFF_RMF(i, jn)                                                                                 \
+  if constexpr (!(CONV_EXP_MODE & 2))                                                                      \
+    acc[i][jn] = mfma32(st == 0 ? cav[i] : AP[gp][jp + D * (i)], bv[pb][jn], acc[i][jn]);
+#define PETDIFF_RRD(dst, off) \
+  if constexpr (!(CONV_EXP_MODE & 64)) dst = *reinterpret_cast<const fragT*>(base + ((off) ^ (g << 5)));
+#define PETDIFF_BRD(dst, ptr) \
+  if constexpr (!(CONV_EXP_MODE & 64)) dst = *reinterpret_cast<const fragT*>(ptr);
+        if (full) {
+          PETDIFF_RMF(0, 0)
+          PETDIFF_RRD(AP[g][j], posoff(j))
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_RMF(0, 1)
+          PETDIFF_BRD(bv[sb][0], pb0)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_RMF(1, 0)
+          PETDIFF_BRD(bv[sb][1], pb1)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_RMF(1, 1)
+          PETDIFF_RRD(AP[g][j + D], posoff(j + D))
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_RMF(2, 0)
+          PETDIFF_RRD(AP[g][j + 2 * D], posoff(j + 2 * D))
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_RMF(2, 1)
+        } else {
+          PETDIFF_RMF(0, 0)
+          PETDIFF_BRD(bv[sb][0], pb0)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_RMF(0, 1)
+          PETDIFF_BRD(bv[sb][1], pb1)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_RMF(1, 0)
+          PETDIFF_RRD(AP[g][j + 2 * D], posoff(j + 2 * D))
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_RMF(1, 1)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_RMF(2, 0)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_RMF(2, 1)
+        }
+#undef PETDIFF_BRD
+#undef PETDIFF_RRD
+#undef PETDIFF_RMF
+        if constexpr (SEG == 2) {
+          if (st == 0 && has_m0) {
+#pragma unroll
+            for (int gg = 0; gg < NG; ++gg) am[gg] = *reinterpret_cast<const fragT*>(base + (amask ^ (gg << 5)));
+          }
+          if (st == 1 && has_m0) {
+#pragma unroll
+            for (int gg = 0; gg < NG; ++gg)
+#pragma unroll
+              for (int jn = 0; jn < 2; ++jn)
+                if constexpr (!(CONV_EXP_MODE & 2)) acc[0][jn] = mfma32(am[gg], epk[gg][jn], acc[0][jn]);
+            const int k2 = kc - dma.n1;
+            if (kc + 1 < NC) load_epk(k2 + 1);
+          }
+        }
+        if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
+#pragma unroll
+          for (int u = 0; u < PPS; ++u) {
+            const int k = st * PPS + u;
+            if (k < NPER) {
+              if constexpr (NEXT == 3) dma.piece2(nbase, k, nkc - dma.n1, lane);
+              else dma.piece1(nbase, k, nkc, lane);
+            } else if (NEXT == 2 && k < NPC) {
+              dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      {
+        constexpr int jl = SEG == 2 ? NT_ - 1 : TAPS - 1;   // the last step's tap (order ends on 5 / 3)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) cav[i] = AP[NG - 1][jl + D * i];
+      }
+    } else if constexpr (sizeof(T) == 2) {
       constexpr int NG = ROWB / 32;
       constexpr int NT_ = SEG == 2 ? G::TAPS2 : TAPS;
       constexpr int NS = NT_ * NG;
@@ -1104,7 +1233,15 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
   }
   }
   if (loader) return;   // s_barrier waits only for the waves still running
-  mfma_bf16(1);   // the last chunk's last step (NS even)
+  if constexpr (REUSE) {   // the last chunk's last step: carried A operands, B in bv[1] (NS even)
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn)
+        if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(cav[i], bv[1][jn], acc[i][jn]);
+  } else {
+    mfma_bf16(1);   // the last chunk's last step (NS even)
+  }
 #if CONV_EXP_MODE & 128
   if constexpr (G::STAGES == 3) {   // diagnostic: main-loop cycles and the clock (s_memrealtime = 100 MHz)
     const unsigned long long st_c1 = __builtin_amdgcn_s_memtime(), st_r1 = __builtin_amdgcn_s_memrealtime();
