@@ -17,7 +17,7 @@ LAYERS = ['down1', 'down2', 'down3', 'up0.conv2', 'up0.block', 'up1.conv2', 'up1
 
 def short(name):
     import re
-    m = re.search(r'conv_kernelI(?:DF16b|f)Li(\d+)E', name)
+    m = re.search(r'conv_kernelI(?:DF16b|DF16_|f)Li(\d+)E', name)
     if m:
         return LAYERS[int(m.group(1))]
     if 'down0_kernel' in name:
