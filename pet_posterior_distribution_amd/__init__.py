@@ -9,6 +9,8 @@ from .helper_func import get_beta_schedule, cos_beta_schedule, chunker
 from .networks import UnetConditional, param_spec, glorot_uniform_init, denoiser_init
 from .diffusion_model import ImprovedDDPM, summarize_stats
 from .training import Adam, ExponentialDecay
+from .checkpoint import TensorBundle, load_unet_weights
 
 __all__ = ['ImprovedDDPM', 'UnetConditional', 'get_beta_schedule', 'cos_beta_schedule', 'chunker',
-           'param_spec', 'glorot_uniform_init', 'denoiser_init', 'summarize_stats', 'Adam', 'ExponentialDecay']
+           'param_spec', 'glorot_uniform_init', 'denoiser_init', 'summarize_stats', 'Adam', 'ExponentialDecay',
+           'TensorBundle', 'load_unet_weights']

@@ -229,5 +229,19 @@ class UnetConditional:
             json.dump({'spec': [[n, list(s)] for n, s in self.spec()]}, f)
 
     def load_weights(self, path):
+        """Weights from this package's .npz, or from a TensorFlow checkpoint of the reference: a SavedModel
+        directory (`cp_<epoch>/`, main_script.py:263) or a TensorBundle prefix (`.../variables/variables`),
+        read by checkpoint.py without TensorFlow.  Keras `.weights.h5` files (main_script.py:412) need an HDF5
+        reader, which this environment lacks."""
+        path = os.fspath(path)
+        if path.endswith('.index'):
+            path = path[:-len('.index')]
+        if os.path.isdir(path) or os.path.exists(path + '.index'):
+            from .checkpoint import load_unet_weights
+            self.set_weights(load_unet_weights(path, self.spec()))
+            return
+        if path.endswith('.h5'):
+            raise NotImplementedError('Keras .weights.h5 (HDF5) is not readable here; pass the SavedModel '
+                                      'checkpoint directory (cp_<epoch>/) instead')
         with np.load(path, allow_pickle=False) as z:
             self.set_weights({n: z[n] for n, _ in self.spec()})
