@@ -146,6 +146,30 @@ def test_p_sample_variants(conds, lv, param):
     m.close()
 
 
+@pytest.mark.parametrize('flag', [True, False])
+def test_loop_fixed_variance_flag_var_tilde(conds, flag):
+    """Fixed variance (learn_variance=''), where var (log beta) and var_tilde (clipped posterior log var)
+    differ: the loop adds var_tilde or var per flag_var_tilde (diffusion_model.py:705-708), graph and
+    eager, vs the oracle with the same injected noise."""
+    m = make_model('float32', seed=21, learn_variance='', final_scale=0.2)
+    rng = np.random.default_rng(22)
+    B = 5
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    idx = R.loop_indices(1000, 12, 'quadratic')        # dense near t = 0, where var and var_tilde differ most
+    z = rng.standard_normal((len(idx), B, 48, 2)).astype(np.float32)
+    out = m.ddpm_loop(x, conds[1:], num_timesteps=12, sub_sequence_type='quadratic', flag_var_tilde=flag, z=z)
+    ref = R.ddpm_loop(m.network.weights, S, x, conds[1:], z, idx, flag_var_tilde=flag, learn_variance='',
+                      dt=np.float64)
+    assert rel(out, ref) < 1e-4
+    other = R.ddpm_loop(m.network.weights, S, x, conds[1:], z, idx, flag_var_tilde=not flag, learn_variance='',
+                        dt=np.float64)
+    assert rel(other, ref) > 5e-4                      # the flag matters in this mode (1.2e-3 here)
+    a = m.ddpm_loop(x, conds[1:], num_timesteps=12, flag_var_tilde=flag, seed=4)
+    b = m.ddpm_loop(x, conds[1:], num_timesteps=12, flag_var_tilde=flag, seed=4, use_graph=False)
+    torch.testing.assert_close(a, b, rtol=0, atol=0)
+    m.close()
+
+
 def test_philox_noise_matches_oracle(m32, conds):
     rng = np.random.default_rng(5)
     B = 4
