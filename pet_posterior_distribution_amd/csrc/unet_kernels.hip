@@ -47,6 +47,13 @@
 #ifndef CONV_TAP_REUSE
 #define CONV_TAP_REUSE 1
 #endif
+// down3 (L = 6, k = 6): a quarter of the (row, tap) products read SAME padding.  With position-major
+// tile rows each fragment is one position of 32 samples, so a whole (fragment, tap) MFMA is either
+// useful or zero; fragments are dealt to the waves so every wave keeps 13 or 14 of 18 and skips the
+// rest (0 = sample-major rows, every tap multiplied).
+#ifndef CONV_DOWN3_PM
+#define CONV_DOWN3_PM 1
+#endif
 
 namespace petdiff {
 
@@ -214,6 +221,15 @@ struct ConvGeom {
   static constexpr int WM = TC.wm, WN = TC.wn, STAGES = TC.stages, ROWB = TC.rowb;
   static constexpr int MT = 96 * WM, NT = 64 * WN;
   static constexpr int S = MT / L;                  // samples per workgroup
+  // down3 position-major (CONV_DOWN3_PM): wave w's fragment i is position pm_pos(w >> 1, i) of samples
+  // 32 (w & 1) .. +31.  Positions {2, 0, 5} keep 13 of the 18 (fragment, tap) products, {3, 1, 4} 14.
+  static constexpr bool PM = CONV_DOWN3_PM && KIND == LK_DOWN3 && sizeof(T) == 2;
+  static constexpr __device__ __host__ int pm_pos(int pat, int i) {
+    return pat == 0 ? (i == 0 ? 2 : i == 1 ? 0 : 5) : (i == 0 ? 3 : i == 1 ? 1 : 4);
+  }
+  static constexpr __device__ __host__ bool pm_valid(int pat, int i, int j) {
+    return pm_pos(pat, i) + j - PADL >= 0 && pm_pos(pat, i) + j - PADL < L;
+  }
   static constexpr int LIN = UPS ? L / 2 : L;       // input rows per sample
   static constexpr int AROWS = S * LIN;
   static constexpr int ZROW = AROWS;                // always-zero LDS row
@@ -281,6 +297,8 @@ struct ConvGeom {
   static constexpr bool LDR = CONV_LOADERS && sizeof(T) == 2 && STAGES == 3 && !FUSED;
   static constexpr int NTH = LDR ? 2 * kThreads : kThreads;
   static_assert(WM * WN == 4, "4 waves");
+  static_assert(!PM || (S == 64 && L == 6 && WM == 4 && WN == 1 && !UPS && !FUSED), "down3 position-major layout");
+  static_assert(!PM || (CONV_LOADERS && STAGES == 3), "position-major down3 runs on the loader-wave ring");
   static_assert(MT % L == 0, "tile must hold whole samples");
   static_assert(B_BYTES % (16 * kThreads) == 0, "B tile split");
   static_assert(ROWB == 64 || ROWB == 128 || (ROWB == 32 && FUSED), "row width");
@@ -304,7 +322,11 @@ struct ConvGeom {
   // (l = 2m + e), so every wave computes one output phase and the m = 0 rows (the only ones
   // whose composite taps need the left-edge correction) fill the first S rows of a phase.
   static __device__ __forceinline__ void row_sl(int r, int& s, int& l) {
-    if constexpr (FUSED) {
+    if constexpr (PM) {
+      const int w = r / 96, i = (r % 96) / 32;
+      l = pm_pos(w >> 1, i);
+      s = (w & 1) * 32 + (r & 31);
+    } else if constexpr (FUSED) {
       s = r % S;
       const int em = r / S, e = em / LH;
       l = 2 * (em - e * LH) + e;
@@ -365,9 +387,9 @@ struct DmaPlan {
       const int c = cp ^ G::key(row);
       // LDS row: (sample, position) = row / LIN, row % LIN; fused: position-major slots
       // (row = li * S + s), so a lane group's 16 samples read 16 consecutive rows
-      const int s = G::FUSED ? row % G::S : row / G::LIN;
+      const int s = (G::FUSED || G::PM) ? row % G::S : row / G::LIN;
       const int q1 = row / G::S;                 // fused: slot1 position index
-      const int li = G::FUSED ? (q1 < G::LH ? 2 * q1 : 2 * (q1 - G::LH) + 1) : row - s * G::LIN;
+      const int li = G::FUSED ? (q1 < G::LH ? 2 * q1 : 2 * (q1 - G::LH) + 1) : G::PM ? q1 : row - s * G::LIN;
       const int b = min(m0 + s, a.B - 1);        // rows of absent samples only feed unstored outputs
       avoff1[qq] = ((b * G::LIN + li) * a.c1 + c * G::EPC) * (int)sizeof(T);
       avoff2[qq] = ((b * G::LIN + li) * a.c2 + c * G::EPC) * (int)sizeof(T);
@@ -647,7 +669,7 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
       const int p = l + j - PADL;
       int row;
       if (G::FUSED) row = (p >= 0 && p < L) ? G::slot1(p, s) : G::ZROW;
-      else if (!UPS) row = (p >= 0 && p < L) ? s * L + p : G::ZROW;
+      else if (!UPS) row = (p >= 0 && p < L) ? (G::PM ? p * G::S + s : s * L + p) : G::ZROW;
       else row = (p < L) ? s * G::LIN + (p >> 1) : G::ZROW;
       aoff[j][i] = (G::FUSED && row == G::ZROW) ? G::ZOFF + (c0 << 4) : row * ROWB + ((c0 ^ G::key(row)) << 4);
     }
@@ -688,6 +710,7 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
     }
   }
   const int wv = __builtin_amdgcn_readfirstlane(w);
+  const int pm_pat = wv >> 1;                       // down3 position-major: this wave's fragment set
 
   f32x16 acc[3][2];
 #pragma unroll
@@ -760,7 +783,7 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
   };
   // NEXT = 2 (first chunk only): the pieces of chunks nkc and nkc + 1 (stages nbuf, nbuf + 1).
   // SEG = 2: a fused segment-2 chunk (4 composite taps of this wave's phase; kc = its index).
-  auto compute = [&](const char* base, auto next_tag, int nkc, int nbuf, auto seg_tag, int kc) {
+  auto compute = [&](const char* base, auto next_tag, int nkc, int nbuf, auto seg_tag, int kc, auto pat_tag) {
     constexpr int NEXT = (int)decltype(next_tag)::value;
     constexpr int SEG = (int)decltype(seg_tag)::value;
     char* nbase = smem + nbuf * G::STAGE;
@@ -877,6 +900,61 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
         constexpr int jl = SEG == 2 ? NT_ - 1 : TAPS - 1;   // the last step's tap (order ends on 5 / 3)
 #pragma unroll
         for (int i = 0; i < 3; ++i) cav[i] = AP[NG - 1][jl + D * i];
+      }
+    } else if constexpr (G::PM) {
+      // position-major down3: step st = (tap j, k-group g); the MFMAs of step st - 1 and the reads
+      // of step st, both over this wave's valid fragments only (pm_valid folds after unrolling)
+      constexpr int NG = ROWB / 32;
+      constexpr int NS = TAPS * NG;
+      constexpr int NPER = G::PER;
+      constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;
+      constexpr int PPS = (NPC + NS - 1) / NS;
+      static_assert(NS % 2 == 0, "fragment double buffer alternates per step");
+      {
+        constexpr int PAT = decltype(pat_tag)::value;
+#pragma unroll
+        for (int st = 0; st < NS; ++st) {
+          const int j = st / NG, g = st % NG, sb = st & 1, pb = sb ^ 1;
+          const int jp = st == 0 ? TAPS - 1 : (st - 1) / NG;   // st = 0: the previous chunk's last step
+          const char* pa0 = base + (aoff[j][0] ^ (g << 5));
+          const char* pa1 = base + (aoff[j][1] ^ (g << 5));
+          const char* pa2 = base + (aoff[j][2] ^ (g << 5));
+          const char* pb0 = base + ((boff[0] + j * NT * ROWB) ^ (g << 5));
+          const char* pb1 = base + ((boff[1] + j * NT * ROWB) ^ (g << 5));
+#define PETDIFF_PMF(i, jn)                                                                                 \
+  if (G::pm_valid(PAT, i, jp)) {                                                                           \
+    if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(av[pb][i], bv[pb][jn], acc[i][jn]);            \
+  }
+#define PETDIFF_PRD(dst, ptr, ok) \
+  if (ok) { if constexpr (!(CONV_EXP_MODE & 64)) dst = *reinterpret_cast<const fragT*>(ptr); }
+          PETDIFF_PMF(0, 0)
+          PETDIFF_PRD(av[sb][0], pa0, G::pm_valid(PAT, 0, j))
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_PMF(0, 1)
+          PETDIFF_PRD(bv[sb][0], pb0, true)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_PMF(1, 0)
+          PETDIFF_PRD(bv[sb][1], pb1, true)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_PMF(1, 1)
+          PETDIFF_PRD(av[sb][1], pa1, G::pm_valid(PAT, 1, j))
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_PMF(2, 0)
+          PETDIFF_PRD(av[sb][2], pa2, G::pm_valid(PAT, 2, j))
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_PMF(2, 1)
+#undef PETDIFF_PRD
+#undef PETDIFF_PMF
+          if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
+#pragma unroll
+            for (int u = 0; u < PPS; ++u) {
+              const int k = st * PPS + u;
+              if (k < NPER) dma.piece1(nbase, k, nkc, lane);
+              else if (NEXT == 2 && k < NPC) dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
     } else if constexpr (sizeof(T) == 2) {
       constexpr int NG = ROWB / 32;
@@ -1006,6 +1084,7 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
   using Yes = std::integral_constant<int, 1>;
   using No = std::integral_constant<int, 0>;
   using Two = std::integral_constant<int, 2>;
+  using P0 = std::integral_constant<int, 0>;   // fragment-set tag (down3 position-major; 0 elsewhere)
 
   // epilogue operands fetched before the K loop (latency hidden behind it)
   const int ep_cg = tid % (NT / 8), ep_nloc = ep_cg * 8;
@@ -1095,47 +1174,47 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
       __syncthreads();
       int kc = 0;
       for (; kc + 1 < n1; ++kc) {
-        compute(smem + (kc & 1) * G::STAGE, Yes{}, kc + 1, (kc + 1) & 1, Seg1{}, 0);
+        compute(smem + (kc & 1) * G::STAGE, Yes{}, kc + 1, (kc + 1) & 1, Seg1{}, 0, P0{});
         wait_vmcnt<0>();
         __syncthreads();
       }
-      compute(smem + (kc & 1) * G::STAGE, Seg2Next{}, kc + 1, (kc + 1) & 1, Seg1{}, 0);
+      compute(smem + (kc & 1) * G::STAGE, Seg2Next{}, kc + 1, (kc + 1) & 1, Seg1{}, 0, P0{});
       wait_vmcnt<0>();
       __syncthreads();
       for (++kc; kc + 1 < NC; ++kc) {
-        compute(smem + (kc & 1) * G::STAGE, Seg2Next{}, kc + 1, (kc + 1) & 1, Seg2{}, kc);
+        compute(smem + (kc & 1) * G::STAGE, Seg2Next{}, kc + 1, (kc + 1) & 1, Seg2{}, kc, P0{});
         wait_vmcnt<0>();
         __syncthreads();
       }
-      compute(smem + (kc & 1) * G::STAGE, No{}, 0, 0, Seg2{}, kc);
+      compute(smem + (kc & 1) * G::STAGE, No{}, 0, 0, Seg2{}, kc, P0{});
       __syncthreads();
     } else {
       dma.all(smem, 0, 0, lane);
       prefetch_maps();
       prefetch_fin_maps();
       ring_barrier<0>();
-      compute(smem, Two{}, 1, 1, Seg1{}, 0);              // chunks 1, 2 -> stages 1, 2
+      compute(smem, Two{}, 1, 1, Seg1{}, 0, P0{});              // chunks 1, 2 -> stages 1, 2
       ring_barrier<G::PER>();
       int buf = 1, kc = 1;
       for (; kc + 2 < n1; ++kc) {
-        compute(smem + buf * G::STAGE, Yes{}, kc + 2, buf == 0 ? 2 : buf - 1, Seg1{}, 0);
+        compute(smem + buf * G::STAGE, Yes{}, kc + 2, buf == 0 ? 2 : buf - 1, Seg1{}, 0, P0{});
         ring_barrier<G::PER>();
         buf = buf == 2 ? 0 : buf + 1;
       }
       for (; kc < n1; ++kc) {                              // the next chunks are segment 2
-        compute(smem + buf * G::STAGE, Seg2Next{}, kc + 2, buf == 0 ? 2 : buf - 1, Seg1{}, 0);
+        compute(smem + buf * G::STAGE, Seg2Next{}, kc + 2, buf == 0 ? 2 : buf - 1, Seg1{}, 0, P0{});
         ring_barrier<G::PER2>();
         buf = buf == 2 ? 0 : buf + 1;
       }
       for (; kc + 2 < NC; ++kc) {
-        compute(smem + buf * G::STAGE, Seg2Next{}, kc + 2, buf == 0 ? 2 : buf - 1, Seg2{}, kc);
+        compute(smem + buf * G::STAGE, Seg2Next{}, kc + 2, buf == 0 ? 2 : buf - 1, Seg2{}, kc, P0{});
         ring_barrier<G::PER2>();
         buf = buf == 2 ? 0 : buf + 1;
       }
-      compute(smem + buf * G::STAGE, No{}, 0, 0, Seg2{}, kc);
+      compute(smem + buf * G::STAGE, No{}, 0, 0, Seg2{}, kc, P0{});
       ring_barrier<0>();
       buf = buf == 2 ? 0 : buf + 1;
-      compute(smem + buf * G::STAGE, No{}, 0, 0, Seg2{}, kc + 1);
+      compute(smem + buf * G::STAGE, No{}, 0, 0, Seg2{}, kc + 1, P0{});
       ring_barrier<0>();
     }
   } else if constexpr (G::STAGES == 2) {
@@ -1144,11 +1223,11 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
     wait_vmcnt<0>();
     __syncthreads();
     for (int kc = 0; kc + 1 < NC; ++kc) {
-      compute(smem + (kc & 1) * G::STAGE, Yes{}, kc + 1, (kc + 1) & 1, Seg1{}, 0);
+      compute(smem + (kc & 1) * G::STAGE, Yes{}, kc + 1, (kc + 1) & 1, Seg1{}, 0, P0{});
       wait_vmcnt<0>();
       __syncthreads();
     }
-    compute(smem + ((NC - 1) & 1) * G::STAGE, No{}, 0, 0, Seg1{}, 0);
+    compute(smem + ((NC - 1) & 1) * G::STAGE, No{}, 0, 0, Seg1{}, 0, P0{});
     __syncthreads();
   } else {
     // 3-deep ring: chunk kc+2 is in flight while chunk kc is computed; the wait
@@ -1173,12 +1252,26 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
       st_c0 = __builtin_amdgcn_s_memtime();
       st_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
-      int buf = 0;
-      for (int kc = 0; kc < NC; ++kc) {
-        compute(smem + buf * G::STAGE, No{}, 0, 0, Seg1{}, 0);
-        ring_barrier<0>();                                 // B(kc+1): own LDS reads done
-        buf = buf == 2 ? 0 : buf + 1;
-      }
+      auto mainloop = [&](auto pat_tag) {
+        int buf = 0;
+        for (int kc = 0; kc < NC; ++kc) {
+          compute(smem + buf * G::STAGE, No{}, 0, 0, Seg1{}, 0, pat_tag);
+          ring_barrier<0>();                               // B(kc+1): own LDS reads done
+          buf = buf == 2 ? 0 : buf + 1;
+        }
+        if constexpr (G::PM) {   // the last step (tap TAPS - 1) of this wave's valid fragments
+          constexpr int PAT = decltype(pat_tag)::value;
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+            if (G::pm_valid(PAT, i, TAPS - 1))
+#pragma unroll
+              for (int jn = 0; jn < 2; ++jn)
+                if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(av[1][i], bv[1][jn], acc[i][jn]);
+        }
+      };
+      // down3 position-major: each fragment set gets its own main loop (no per-chunk branch)
+      if (G::PM && pm_pat != 0) mainloop(std::integral_constant<int, 1>{});
+      else mainloop(P0{});
     }
   } else {
     // bf16: the prologue lands chunk 0 only; chunk 0's compute issues chunks 1 and 2.
@@ -1203,10 +1296,10 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
     int buf = 0, kc = 0;
     if constexpr (EARLY) {
       if (NC >= 3) {
-        compute(smem, Two{}, 1, 1, Seg1{}, 0);                    // chunks 1, 2 -> stages 1, 2
+        compute(smem, Two{}, 1, 1, Seg1{}, 0, P0{});                    // chunks 1, 2 -> stages 1, 2
         ring_barrier<G::PER>();
       } else if (NC == 2) {
-        compute(smem, Yes{}, 1, 1, Seg1{}, 0);
+        compute(smem, Yes{}, 1, 1, Seg1{}, 0, P0{});
         ring_barrier<0>();
       }
       if (NC >= 2) {
@@ -1216,18 +1309,18 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
     }
     for (; kc + 2 < NC; ++kc) {
       const int nb = buf == 0 ? 2 : buf - 1;          // (kc + 2) % 3
-      compute(smem + buf * G::STAGE, Yes{}, kc + 2, nb, Seg1{}, 0);
+      compute(smem + buf * G::STAGE, Yes{}, kc + 2, nb, Seg1{}, 0, P0{});
       ring_barrier<G::PER>();
       buf = buf == 2 ? 0 : buf + 1;
     }
     // tail: the last (up to) two chunks, nothing left to prefetch
     if (kc + 1 < NC) {
-      compute(smem + buf * G::STAGE, No{}, 0, 0, Seg1{}, 0);
+      compute(smem + buf * G::STAGE, No{}, 0, 0, Seg1{}, 0, P0{});
       ring_barrier<0>();
       buf = buf == 2 ? 0 : buf + 1;
     }
     if (kc < NC) {
-      compute(smem + buf * G::STAGE, No{}, 0, 0, Seg1{}, 0);
+      compute(smem + buf * G::STAGE, No{}, 0, 0, Seg1{}, 0, P0{});
       ring_barrier<0>();
     }
   }
@@ -1239,6 +1332,8 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
 #pragma unroll
       for (int jn = 0; jn < 2; ++jn)
         if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(cav[i], bv[1][jn], acc[i][jn]);
+  } else if constexpr (G::PM) {
+    // flushed at the end of the position-major main loop
   } else {
     mfma_bf16(1);   // the last chunk's last step (NS even)
   }
@@ -1315,8 +1410,9 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
       for (int k = 0; k < 4; ++k) cq[k] = *reinterpret_cast<const f32x4*>(ct + rp * G::CT_LD + nloc * 2 + 4 * k);
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        const int se = G::FUSED ? s + e : s, le = G::FUSED ? l : l + e, be = m0 + se;
-        if (G::FUSED && !FAST && be >= B) continue;
+        constexpr bool SPAIR = G::FUSED || G::PM;   // the pair is two samples at one position
+        const int se = SPAIR ? s + e : s, le = SPAIR ? l : l + e, be = m0 + se;
+        if (SPAIR && !FAST && be >= B) continue;
         const f32x4 c0v = {cq[0][e], cq[0][2 + e], cq[1][e], cq[1][2 + e]};
         const f32x4 c1v = {cq[2][e], cq[2][2 + e], cq[3][e], cq[3][2 + e]};
         f32x4 m0v = ep_b0, m1v = ep_b1;
