@@ -22,6 +22,10 @@ def short(name):
         return LAYERS[int(m.group(1))]
     if 'down0_kernel' in name:
         return 'down0'
+    # rocprofv3 demangles conv_kernel<__bf16, 1> as 'conv_kernel<bool _Accum, int, E>'; of the 16-bit
+    # conv kinds a generate launches (0, 1, 2, 9, 10, 11) only kind 1 (down2) comes out that way
+    if 'conv_kernel<bool _Accum, int, E>' in name:
+        return 'down2'
     return None
 
 
