@@ -47,12 +47,18 @@
 #ifndef CONV_TAP_REUSE
 #define CONV_TAP_REUSE 1
 #endif
-// down3 (L = 6, k = 6): a quarter of the (row, tap) products read SAME padding.  With position-major
-// tile rows each fragment is one position of 32 samples, so a whole (fragment, tap) MFMA is either
-// useful or zero; fragments are dealt to the waves so every wave keeps 13 or 14 of 18 and skips the
-// rest (0 = sample-major rows, every tap multiplied).
+// down3 (L = 6, k = 6): a quarter of the (row, tap) products read SAME padding; down2 (L = 12): 1/8.
+// With position-major tile rows each fragment is one position of 32 samples, so a whole (fragment,
+// tap) MFMA is either useful or zero; fragments are dealt to the waves so every wave keeps 13 or 14
+// (down3) / 15 or 16 (down2) of 18 and skips the rest, and a fragment's lanes read consecutive LDS
+// rows (0 = sample-major rows, every tap multiplied).
 #ifndef CONV_DOWN3_PM
 #define CONV_DOWN3_PM 1
+#endif
+// down2 position-major (its 4 fragment sets keep 16/16/16/15 of 18): bitwise equal, but measured
+// slower (A/B 4713 vs 4775 samples/s, down2 21.6 vs 19.5 us), so off; see DESIGN.md section 3
+#ifndef CONV_DOWN2_PM
+#define CONV_DOWN2_PM 0
 #endif
 
 namespace petdiff {
@@ -221,14 +227,33 @@ struct ConvGeom {
   static constexpr int WM = TC.wm, WN = TC.wn, STAGES = TC.stages, ROWB = TC.rowb;
   static constexpr int MT = 96 * WM, NT = 64 * WN;
   static constexpr int S = MT / L;                  // samples per workgroup
-  // down3 position-major (CONV_DOWN3_PM): wave w's fragment i is position pm_pos(w >> 1, i) of samples
-  // 32 (w & 1) .. +31.  Positions {2, 0, 5} keep 13 of the 18 (fragment, tap) products, {3, 1, 4} 14.
-  static constexpr bool PM = CONV_DOWN3_PM && KIND == LK_DOWN3 && sizeof(T) == 2;
+  // Position-major down layers (CONV_DOWN3_PM, CONV_DOWN2_PM): wave w's fragment i is position
+  // pm_pos(w / SH, i) of samples 32 (w % SH) .. +31 (SH = sample halves per tile).
+  //   down3 (L = 6, S = 64): {2, 0, 5} keep 13 of the 18 (fragment, tap) products, {3, 1, 4} 14.
+  //   down2 (L = 12, S = 32): {0, 2, 3}, {10, 4, 5}, {1, 9, 6} keep 16, {11, 7, 8} 15.
+  static constexpr bool PM = sizeof(T) == 2 && ((CONV_DOWN3_PM && KIND == LK_DOWN3) ||
+                                                (CONV_DOWN2_PM && KIND == LK_DOWN2));
+  static constexpr int SH = PM ? S / 32 : 1;        // sample halves (waves per fragment set)
+  static constexpr int NPAT = 4 / SH;               // fragment sets
   static constexpr __device__ __host__ int pm_pos(int pat, int i) {
-    return pat == 0 ? (i == 0 ? 2 : i == 1 ? 0 : 5) : (i == 0 ? 3 : i == 1 ? 1 : 4);
+    if (L == 6) return pat == 0 ? (i == 0 ? 2 : i == 1 ? 0 : 5) : (i == 0 ? 3 : i == 1 ? 1 : 4);
+    return pat == 0 ? (i == 0 ? 0 : i == 1 ? 2 : 3)
+         : pat == 1 ? (i == 0 ? 10 : i == 1 ? 4 : 5)
+         : pat == 2 ? (i == 0 ? 1 : i == 1 ? 9 : 6)
+                    : (i == 0 ? 11 : i == 1 ? 7 : 8);
   }
   static constexpr __device__ __host__ bool pm_valid(int pat, int i, int j) {
     return pm_pos(pat, i) + j - PADL >= 0 && pm_pos(pat, i) + j - PADL < L;
+  }
+  // tile row of (position l, sample s): the inverse of row_sl
+  static __device__ __forceinline__ int pm_row(int l, int s) {
+    int r = 0;
+#pragma unroll
+    for (int pat = 0; pat < NPAT; ++pat)
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if (pm_pos(pat, i) == l) r = (pat * SH + (s >> 5)) * 96 + i * 32 + (s & 31);
+    return r;
   }
   static constexpr int LIN = UPS ? L / 2 : L;       // input rows per sample
   static constexpr int AROWS = S * LIN;
@@ -297,8 +322,9 @@ struct ConvGeom {
   static constexpr bool LDR = CONV_LOADERS && sizeof(T) == 2 && STAGES == 3 && !FUSED;
   static constexpr int NTH = LDR ? 2 * kThreads : kThreads;
   static_assert(WM * WN == 4, "4 waves");
-  static_assert(!PM || (S == 64 && L == 6 && WM == 4 && WN == 1 && !UPS && !FUSED), "down3 position-major layout");
-  static_assert(!PM || (CONV_LOADERS && STAGES == 3), "position-major down3 runs on the loader-wave ring");
+  static_assert(!PM || (((S == 64 && L == 6) || (S == 32 && L == 12)) && WM == 4 && WN == 1 && !UPS && !FUSED),
+                "position-major layout: 3 positions of 32 samples per wave");
+  static_assert(!PM || (CONV_LOADERS && STAGES == 3), "position-major layers run on the loader-wave ring");
   static_assert(MT % L == 0, "tile must hold whole samples");
   static_assert(B_BYTES % (16 * kThreads) == 0, "B tile split");
   static_assert(ROWB == 64 || ROWB == 128 || (ROWB == 32 && FUSED), "row width");
@@ -324,8 +350,8 @@ struct ConvGeom {
   static __device__ __forceinline__ void row_sl(int r, int& s, int& l) {
     if constexpr (PM) {
       const int w = r / 96, i = (r % 96) / 32;
-      l = pm_pos(w >> 1, i);
-      s = (w & 1) * 32 + (r & 31);
+      l = pm_pos(w / SH, i);
+      s = (w % SH) * 32 + (r & 31);
     } else if constexpr (FUSED) {
       s = r % S;
       const int em = r / S, e = em / LH;
@@ -710,7 +736,7 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
     }
   }
   const int wv = __builtin_amdgcn_readfirstlane(w);
-  const int pm_pat = wv >> 1;                       // down3 position-major: this wave's fragment set
+  const int pm_pat = wv / G::SH;                    // position-major: this wave's fragment set
 
   f32x16 acc[3][2];
 #pragma unroll
@@ -1269,9 +1295,18 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
                 if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(av[1][i], bv[1][jn], acc[i][jn]);
         }
       };
-      // down3 position-major: each fragment set gets its own main loop (no per-chunk branch)
-      if (G::PM && pm_pat != 0) mainloop(std::integral_constant<int, 1>{});
-      else mainloop(P0{});
+      // position-major: each fragment set gets its own main loop (no per-chunk branch)
+      if constexpr (G::PM && G::NPAT == 4) {
+        if (pm_pat == 0) mainloop(P0{});
+        else if (pm_pat == 1) mainloop(std::integral_constant<int, 1>{});
+        else if (pm_pat == 2) mainloop(std::integral_constant<int, 2>{});
+        else mainloop(std::integral_constant<int, 3>{});
+      } else if constexpr (G::PM) {
+        if (pm_pat != 0) mainloop(std::integral_constant<int, 1>{});
+        else mainloop(P0{});
+      } else {
+        mainloop(P0{});
+      }
     }
   } else {
     // bf16: the prologue lands chunk 0 only; chunk 0's compute issues chunks 1 and 2.
@@ -1396,63 +1431,88 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
     auto epi_rows = [&](auto mode_tag) {
       constexpr int MODE = decltype(mode_tag)::value;
       constexpr bool FAST = MODE != 0;
+      constexpr bool SPAIR = G::FUSED || G::PM;   // a row pair is two samples at one position
+      // row pair rp = tile rows (2 rp, 2 rp + 1) = (sample s, position l) and its partner
+      // (s, l + 1), or (SPAIR) (s + 1, l): + maps, act, 16-B stores; the two rows' values -> v
+      auto pair = [&](int rp, int s, int l, float (&v)[2][8]) {
+        f32x4 cq[4];   // (r, r+1) x channels nloc .. nloc+7, interleaved
 #pragma unroll
-    for (int rp = tid / TPR; rp < G::MT / 2; rp += kThreads / TPR) {
-      // the pair (r, r + 1): positions (l, l + 1) of sample s, or (fused) samples (s, s + 1) at l
-      const int r = 2 * rp;
-      int s, l;
-      G::row_sl(r, s, l);
-      const int b = m0 + s;
-      if (!FAST && b >= B) continue;
-      float v[2][8];
-      f32x4 cq[4];   // (r, r+1) x channels nloc .. nloc+7, interleaved
+        for (int k = 0; k < 4; ++k) cq[k] = *reinterpret_cast<const f32x4*>(ct + rp * G::CT_LD + nloc * 2 + 4 * k);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) cq[k] = *reinterpret_cast<const f32x4*>(ct + rp * G::CT_LD + nloc * 2 + 4 * k);
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        constexpr bool SPAIR = G::FUSED || G::PM;   // the pair is two samples at one position
-        const int se = SPAIR ? s + e : s, le = SPAIR ? l : l + e, be = m0 + se;
-        if (SPAIR && !FAST && be >= B) continue;
-        const f32x4 c0v = {cq[0][e], cq[0][2 + e], cq[1][e], cq[1][2 + e]};
-        const f32x4 c1v = {cq[2][e], cq[2][2 + e], cq[3][e], cq[3][2 + e]};
-        f32x4 m0v = ep_b0, m1v = ep_b1;
-        if constexpr (MODE == 1) {
-          m0v = *reinterpret_cast<const f32x4*>(lt + le * NT + nloc) +
-                *reinterpret_cast<const f32x4*>(lc + le * NT + nloc);
-          m1v = *reinterpret_cast<const f32x4*>(lt + le * NT + nloc + 4) +
-                *reinterpret_cast<const f32x4*>(lc + le * NT + nloc + 4);
-        } else if constexpr (MODE == 0) {
-          const int tac = stac[se];
-          if (a.tmap) {
-            const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[be];
-            const float* mp = a.tmap + ((size_t)t * L + le) * cout + n;
-            m0v = *reinterpret_cast<const f32x4*>(mp);
-            m1v = *reinterpret_cast<const f32x4*>(mp + 4);
+        for (int e = 0; e < 2; ++e) {
+          const int se = SPAIR ? s + e : s, le = SPAIR ? l : l + e, be = m0 + se;
+          if (SPAIR && !FAST && be >= B) continue;
+          const f32x4 c0v = {cq[0][e], cq[0][2 + e], cq[1][e], cq[1][2 + e]};
+          const f32x4 c1v = {cq[2][e], cq[2][2 + e], cq[3][e], cq[3][2 + e]};
+          f32x4 m0v = ep_b0, m1v = ep_b1;
+          if constexpr (MODE == 1) {
+            m0v = *reinterpret_cast<const f32x4*>(lt + le * NT + nloc) +
+                  *reinterpret_cast<const f32x4*>(lc + le * NT + nloc);
+            m1v = *reinterpret_cast<const f32x4*>(lt + le * NT + nloc + 4) +
+                  *reinterpret_cast<const f32x4*>(lc + le * NT + nloc + 4);
+          } else if constexpr (MODE == 0) {
+            const int tac = stac[se];
+            if (a.tmap) {
+              const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[be];
+              const float* mp = a.tmap + ((size_t)t * L + le) * cout + n;
+              m0v = *reinterpret_cast<const f32x4*>(mp);
+              m1v = *reinterpret_cast<const f32x4*>(mp + 4);
+            }
+            if (a.cmap) {
+              const float* cp = a.cmap + ((size_t)tac * L + le) * cout + n;
+              m0v += *reinterpret_cast<const f32x4*>(cp);
+              m1v += *reinterpret_cast<const f32x4*>(cp + 4);
+            }
           }
-          if (a.cmap) {
-            const float* cp = a.cmap + ((size_t)tac * L + le) * cout + n;
-            m0v += *reinterpret_cast<const f32x4*>(cp);
-            m1v += *reinterpret_cast<const f32x4*>(cp + 4);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            v[e][q] = c0v[q] + m0v[q];
+            v[e][4 + q] = c1v[q] + m1v[q];
+          }
+          if constexpr (EPI != EPI_LIN) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[e][q] = fmaxf(v[e][q], 0.f);
+          }
+          if (!FAST || be < B) Vec8<T>::store(a.out + ((size_t)be * L + le) * cout + n, v[e]);
+        }
+      };
+      if constexpr (G::PM && EPI == EPI_POOL) {
+        // position-major pooling: a quad = samples (s, s + 1) at positions (2 p, 2 p + 1), two row pairs
+        static_assert((G::MT / 4) % (kThreads / TPR) == 0, "quads split evenly");
+#pragma unroll
+        for (int qd = tid / TPR; qd < G::MT / 4; qd += kThreads / TPR) {
+          const int p = qd / (G::S / 2), s = 2 * (qd % (G::S / 2));
+          if (!FAST && m0 + s >= B) continue;
+          float v0[2][8], v1[2][8];
+          pair(G::pm_row(2 * p, s) >> 1, s, 2 * p, v0);
+          pair(G::pm_row(2 * p + 1, s) >> 1, s, 2 * p + 1, v1);
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            float pv[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) pv[q] = fmaxf(v0[e][q], v1[e][q]);
+            if (m0 + s + e < B) Vec8<T>::store(a.out_pool + ((size_t)(m0 + s + e) * (L / 2) + p) * cout + n, pv);
           }
         }
+      } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          v[e][q] = c0v[q] + m0v[q];
-          v[e][4 + q] = c1v[q] + m1v[q];
+        for (int rp = tid / TPR; rp < G::MT / 2; rp += kThreads / TPR) {
+          const int r = 2 * rp;
+          int s, l;
+          G::row_sl(r, s, l);
+          const int b = m0 + s;
+          if (!FAST && b >= B) continue;
+          float v[2][8];
+          pair(rp, s, l, v);
+          if constexpr (EPI == EPI_POOL) {
+            static_assert(!SPAIR || EPI != EPI_POOL, "pooled pairs are two positions of one sample");
+            float pv[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) pv[q] = fmaxf(v[0][q], v[1][q]);
+            if (!FAST || b < B) Vec8<T>::store(a.out_pool + ((size_t)b * (L / 2) + (l >> 1)) * cout + n, pv);
+          }
         }
-        if constexpr (EPI != EPI_LIN) {
-#pragma unroll
-          for (int q = 0; q < 8; ++q) v[e][q] = fmaxf(v[e][q], 0.f);
-        }
-        if (!FAST || be < B) Vec8<T>::store(a.out + ((size_t)be * L + le) * cout + n, v[e]);
       }
-      if constexpr (EPI == EPI_POOL) {
-        float pv[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) pv[q] = fmaxf(v[0][q], v[1][q]);
-        if (!FAST || b < B) Vec8<T>::store(a.out_pool + ((size_t)b * (L / 2) + (l >> 1)) * cout + n, pv);
-      }
-    }
     };
     if (mode == 1) epi_rows(std::integral_constant<int, 1>{});
     else if (mode == 2) epi_rows(std::integral_constant<int, 2>{});
