@@ -37,6 +37,9 @@ UP0_CONV2_FLOP_PER_SAMPLE = 2 * 12 * 2 * 1074 * 512
 UP0_FUSED_EXEC_FLOP_PER_SAMPLE = 2 * 12 * 512 * 512 * 6 + 2 * 12 * 4 * 1024 * 512 + 2 * 2 * 1024 * 512
 PEAK_BF16_TFLOPS = 2500.0                   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0                       # HBM3E (MI355X_MICROARCH.md)
+PEAK_CLOCK_HZ = 2.4e9                       # engine clock the dense MFMA peak is quoted at
+N_SIMD = 256 * 4                            # 256 CUs x 4 SIMDs
 # training step: forward + data grad + weight grad of every layer, incl. the
 # per-sample condition encoder / label projections / time MLP (6,002,304 FLOP per sample forward)
 TRAIN_FLOP_PER_SAMPLE = 3 * (FLOP_PER_SAMPLE_STEP + 6_002_304)
@@ -154,16 +157,38 @@ def cpu_baseline(weights, cond, budget_s=15.0):
                       f'extrapolated to 1000 steps'}
 
 
-def load_traffic(fused_up=False):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
-    (None when that kernel has no PMC pass on record)."""
+def load_pmc(fused_up=False):
+    """Per-launch PMC figures of the dominant kernel from the committed rocprofv3 summary
+    (profiles/pmc_traffic.json): HBM bytes (FETCH_SIZE x2 + WRITE_SIZE), SQ_VALU_MFMA_BUSY_CYCLES
+    and GRBM_GUI_ACTIVE; missing entries are None."""
+    pre = 'up0_fused' if fused_up else 'up0_block'
     p = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     try:
         with open(p) as f:
             d = json.load(f)
-        return d.get('up0_fused_bytes_per_launch' if fused_up else 'up0_block_bytes_per_launch')
     except Exception:
-        return None
+        d = {}
+    return {k: d.get(pre + suf) for k, suf in (('traffic', '_bytes_per_launch'), ('mfma_busy', '_mfma_busy_cycles'),
+                                                ('grbm', '_grbm_gui_active'), ('source', '_source'))}
+
+
+def pmc_fields(pmc, avg_s):
+    """HBM GB/s and MFMA utilisation of the dominant kernel against chip peak.
+    SQ_VALU_MFMA_BUSY_CYCLES = 32 cycles per 32x32x16 MFMA (MI355X_MICROARCH.md), summed over the
+    1024 SIMDs.  mfma_util = busy / (1024 x 2.4 GHz x launch time): the MFMA pipes' share of the
+    peak-clock cycles (the same ratio as executed FLOP/s / dense peak).  mfma_busy_vs_active divides
+    by the kernel's own active cycles instead (GRBM_GUI_ACTIVE / 8 XCDs), which the guide notes
+    reads high on dispatches this short, so that fraction reads low."""
+    out = {'hbm_gbs': None, 'hbm_frac': None, 'mfma_util': None, 'mfma_busy_vs_active': None}
+    if pmc['traffic']:
+        out['hbm_gbs'] = round(pmc['traffic'] / avg_s / 1e9, 1)
+        out['hbm_frac'] = round(pmc['traffic'] / avg_s / 1e9 / PEAK_HBM_GBS, 4)
+    if pmc['mfma_busy']:
+        out['mfma_util'] = round(pmc['mfma_busy'] / (N_SIMD * PEAK_CLOCK_HZ * avg_s), 4)
+        if pmc['grbm']:
+            out['mfma_busy_vs_active'] = round(pmc['mfma_busy'] / (N_SIMD * pmc['grbm'] / 8), 4)
+    out['pmc_source'] = pmc['source']
+    return out
 
 
 # MH cost per element update (one ROI's SRTM2 + 54 truncated-normal terms), counted
@@ -446,14 +471,17 @@ def main():
             alg = UP0_BLOCK_FLOP_PER_SAMPLE + (UP0_CONV2_FLOP_PER_SAMPLE if fused_up else 0)
             exe = UP0_FUSED_EXEC_FLOP_PER_SAMPLE if fused_up else UP0_BLOCK_EXEC_FLOP_PER_SAMPLE
             ach = alg * bt / avg_s / 1e12
+            # the PMC passes are taken at B = 1024, bf16 (config 2); other launch sizes / dtypes get none
+            pmc = load_pmc(fused_up) if (bt == 1024 and args.dtype == 'bfloat16') else {'traffic': None, 'mfma_busy': None, 'grbm': None, 'source': None}
             kname = ('conv_kernel<up0 fused> (UpSampling1D + k2 conv 1074->512 + ConvBlock 1024->512 k6+res, L=12)'
                      if fused_up else 'conv_kernel<up0.block> (L=12, 1024->512, k6+res)')
             roof = {'bound': 'mfma', 'kernel': kname,
                     'achieved': round(ach, 2), 'peak': peak, 'unit': 'TFLOP/s', 'frac': round(ach / peak, 4),
-                    'traffic': load_traffic(fused_up) if bt == 1024 else None, 'avg_launch_us': round(avg_s * 1e6, 2),
+                    'traffic': pmc['traffic'], 'avg_launch_us': round(avg_s * 1e6, 2),
                     'executed_tflops': round(exe * bt / avg_s / 1e12, 2),
                     'pipeline_tflops': round(tflops_pipeline, 2),
                     'pipeline_frac': round(tflops_pipeline / peak, 4)}
+            roof.update(pmc_fields(pmc, avg_s))
         line = {
             'metric': 'posterior samples/sec (48-ROI TAC, 1000-step reverse) at 1/2/4/8 MI355X',
             'value': round(value, 2), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,

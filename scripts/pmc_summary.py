@@ -58,6 +58,9 @@ def main(d, out=None):
                 tr[pre + '_read_bytes'] = ub['hbm_read_bytes_corrected']
                 tr[pre + '_write_bytes'] = ub['hbm_write_bytes']
                 tr[pre + '_source'] = os.path.relpath(out, root)
+            for c, name in (('SQ_VALU_MFMA_BUSY_CYCLES', '_mfma_busy_cycles'), ('GRBM_GUI_ACTIVE', '_grbm_gui_active')):
+                if c in ub:
+                    tr[pre + name] = ub[c]
         tr['method'] = 'rocprofv3 --pmc FETCH_SIZE (x2, gfx950 64-B tally) + WRITE_SIZE, KB->B, mean per dispatch'
         json.dump(tr, open(tp, 'w'), indent=1)
     return res

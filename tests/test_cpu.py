@@ -325,3 +325,20 @@ def test_fused_up_composite_identity():
             if m == 0:
                 yc[l] += b[0] @ C[8 + e]
         np.testing.assert_allclose(yc, y, rtol=1e-12, atol=1e-12)
+
+
+def test_bench_pmc_fields_known_answer():
+    """bench.py's PMC-derived roofline extras: HBM GB/s vs 8 TB/s, and MFMA utilisation from
+    SQ_VALU_MFMA_BUSY_CYCLES (32 cycles per 32x32x16 MFMA over 1024 SIMDs at 2.4 GHz), which
+    must equal executed FLOP/s / dense peak (32768 FLOP per MFMA -> 1024 FLOP per busy cycle)."""
+    import bench
+    n_mfma = 1_000_000
+    pmc = {'traffic': 8e12 * 1e-4, 'mfma_busy': 32 * n_mfma, 'grbm': 8 * 100_000, 'source': 'x'}
+    f = bench.pmc_fields(pmc, 1e-4)
+    assert f['hbm_gbs'] == 8000.0 and f['hbm_frac'] == 1.0
+    exe_tflops = n_mfma * 32768 / 1e-4 / 1e12
+    # 2.5 PF / (1024 SIMDs x 2.4 GHz) = 1017 FLOP per SIMD-cycle vs the MFMA's 1024: 0.7% apart
+    assert abs(f['mfma_util'] / (exe_tflops / bench.PEAK_BF16_TFLOPS) - 1) < 0.01
+    assert f['mfma_busy_vs_active'] == round(32 * n_mfma / (1024 * 100_000), 4)
+    none = bench.pmc_fields({'traffic': None, 'mfma_busy': None, 'grbm': None, 'source': None}, 1e-4)
+    assert none['hbm_gbs'] is None and none['mfma_util'] is None
