@@ -210,6 +210,26 @@ def test_loop_full_1000_steps_f32(m32, conds):
     assert rel(out, ref) < 1e-4
 
 
+def test_config1_posterior_mean_sd_f32(m32, conds):
+    """BASELINE configs[0] exactly: one TAC, 48 ROI, n_posterior = 32, 100-step linear sub-sequence
+    (main_script.py:419-436).  Same x_T and injected noise as the fp64 oracle; the per-ROI posterior
+    mean and population SD (ddof = 0, main_script.py:433-436), computed on the GPU by
+    posterior_stats, match the oracle's NumPy moments within the north star's 1e-4 rtol."""
+    rng = np.random.default_rng(31)
+    B = 32
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    idx = R.loop_indices(1000, 100, 'linear')
+    z = rng.standard_normal((len(idx), B, 48, 2)).astype(np.float32)
+    out = m32.ddpm_loop(x, conds[:1], num_timesteps=100, sub_sequence_type='linear', z=z)
+    ref = R.ddpm_loop(m32.network.weights, S, x, conds[:1], z, idx, dt=np.float64)
+    assert rel(out, ref) < 1e-4
+    st = m32.posterior_stats(out)[0]                     # (48, 2, [count, mean, M2])
+    mean_ref, sd_ref = ref.mean(0), ref.std(0)
+    assert rel(st[..., 1], mean_ref) < 1e-4
+    assert rel(np.sqrt(st[..., 2] / B), sd_ref) < 1e-4
+    np.testing.assert_allclose(np.sqrt(st[..., 2] / B), sd_ref, rtol=1e-4, atol=1e-4 * sd_ref.max())
+
+
 def test_keep_all_xt(m32, conds):
     rng = np.random.default_rng(8)
     x = rng.standard_normal((3, 48, 2)).astype(np.float32)
