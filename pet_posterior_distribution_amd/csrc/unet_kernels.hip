@@ -55,10 +55,10 @@
 #ifndef CONV_DOWN3_PM
 #define CONV_DOWN3_PM 1
 #endif
-// down2 position-major (its 4 fragment sets keep 16/16/16/15 of 18): bitwise equal, but measured
-// slower (A/B 4713 vs 4775 samples/s, down2 21.6 vs 19.5 us), so off; see DESIGN.md section 3
+// down2 position-major (its 4 fragment sets keep 16/16/16/15 of 18): bitwise equal to sample-major;
+// down2 18.40 vs 18.64 us once the prologue's row offsets use the wave-uniform set
 #ifndef CONV_DOWN2_PM
-#define CONV_DOWN2_PM 0
+#define CONV_DOWN2_PM 1
 #endif
 
 namespace petdiff {
@@ -235,25 +235,26 @@ struct ConvGeom {
                                                 (CONV_DOWN2_PM && KIND == LK_DOWN2));
   static constexpr int SH = PM ? S / 32 : 1;        // sample halves (waves per fragment set)
   static constexpr int NPAT = 4 / SH;               // fragment sets
+  // fragment set pat, fragment i -> position, packed 4 bits per entry (index 3 pat + i), so a
+  // runtime lookup is one shift and one mask, not a select chain
+  static constexpr unsigned long long PM_TAB = L == 6 ? 0x413502ull : 0x87B69154A320ull;
   static constexpr __device__ __host__ int pm_pos(int pat, int i) {
-    if (L == 6) return pat == 0 ? (i == 0 ? 2 : i == 1 ? 0 : 5) : (i == 0 ? 3 : i == 1 ? 1 : 4);
-    return pat == 0 ? (i == 0 ? 0 : i == 1 ? 2 : 3)
-         : pat == 1 ? (i == 0 ? 10 : i == 1 ? 4 : 5)
-         : pat == 2 ? (i == 0 ? 1 : i == 1 ? 9 : 6)
-                    : (i == 0 ? 11 : i == 1 ? 7 : 8);
+    return (int)((PM_TAB >> (4 * (3 * pat + i))) & 15);
   }
   static constexpr __device__ __host__ bool pm_valid(int pat, int i, int j) {
     return pm_pos(pat, i) + j - PADL >= 0 && pm_pos(pat, i) + j - PADL < L;
   }
+  // position -> 3 pat + i (the inverse table)
+  static constexpr unsigned long long pm_inv_tab() {
+    unsigned long long t = 0;
+    for (int k = 0; k < 3 * NPAT; ++k) t |= (unsigned long long)k << (4 * pm_pos(k / 3, k % 3));
+    return t;
+  }
+  static constexpr unsigned long long PM_INV = pm_inv_tab();
   // tile row of (position l, sample s): the inverse of row_sl
   static __device__ __forceinline__ int pm_row(int l, int s) {
-    int r = 0;
-#pragma unroll
-    for (int pat = 0; pat < NPAT; ++pat)
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-        if (pm_pos(pat, i) == l) r = (pat * SH + (s >> 5)) * 96 + i * 32 + (s & 31);
-    return r;
+    const int k = (int)((PM_INV >> (4 * l)) & 15), pat = k / 3, i = k - 3 * pat;
+    return (pat * SH + (s >> 5)) * 96 + i * 32 + (s & 31);
   }
   static constexpr int LIN = UPS ? L / 2 : L;       // input rows per sample
   static constexpr int AROWS = S * LIN;
@@ -684,6 +685,8 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
 
   // per-lane LDS byte offsets of the A fragment rows (tap j, m-subtile i) and B rows
   const int c0 = (sizeof(T) == 2) ? h : 2 * h;
+  const int wv = __builtin_amdgcn_readfirstlane(w);
+  const int pm_pat = wv / G::SH;                    // position-major: this wave's fragment set
   int aoff[TAPS][3];
 #pragma unroll
   for (int j = 0; j < TAPS; ++j) {
@@ -691,7 +694,12 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
     for (int i = 0; i < 3; ++i) {
       const int r = wm * 96 + i * 32 + lr;
       int s, l;
-      G::row_sl(r, s, l);
+      if constexpr (G::PM) {   // wave-uniform position: scalar work, no divergent select chain
+        l = G::pm_pos(pm_pat, i);
+        s = (wv % G::SH) * 32 + lr;
+      } else {
+        G::row_sl(r, s, l);
+      }
       const int p = l + j - PADL;
       int row;
       if (G::FUSED) row = (p >= 0 && p < L) ? G::slot1(p, s) : G::ZROW;
@@ -735,8 +743,6 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
       boff2[jn] = G::A2_BYTES + (ph * G::TAPS2 * NT + n) * ROWB + ((c0 ^ G::key(n)) << 4);
     }
   }
-  const int wv = __builtin_amdgcn_readfirstlane(w);
-  const int pm_pat = wv / G::SH;                    // position-major: this wave's fragment set
 
   f32x16 acc[3][2];
 #pragma unroll
