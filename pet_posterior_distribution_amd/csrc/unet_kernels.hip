@@ -409,7 +409,9 @@ struct DmaPlan {
 #pragma unroll
     for (int qq = 0; qq < G::APT; ++qq) {
       int p = qq * kThreads + wv * 64 + lane;
-      if (p >= G::APIECES) p = G::APIECES - 1;   // inactive lanes of a partial last instruction
+      // inactive lanes of a partial last instruction (compiled out when the pieces fill whole
+      // instructions, so the per-piece math stays affine in qq and folds)
+      if (G::APIECES % kThreads != 0 && p >= G::APIECES) p = G::APIECES - 1;
       const int row = p / G::CPR, cp = p - row * G::CPR;
       const int c = cp ^ G::key(row);
       // LDS row: (sample, position) = row / LIN, row % LIN; fused: position-major slots
@@ -425,7 +427,7 @@ struct DmaPlan {
 #pragma unroll
       for (int qq = 0; qq < G::APT2; ++qq) {
         int p = qq * kThreads + wv * 64 + lane;
-        if (p >= G::APIECES2) p = G::APIECES2 - 1;
+        if (G::APIECES2 % kThreads != 0 && p >= G::APIECES2) p = G::APIECES2 - 1;
         const int row = p / G::CPR, cp = p - row * G::CPR;
         const int c = cp ^ G::key(row);
         const int s = row % G::S, li = row / G::S;
