@@ -57,6 +57,10 @@
 #endif
 // down2 position-major (its 4 fragment sets keep 16/16/16/15 of 18): bitwise equal to sample-major;
 // down2 18.40 vs 18.64 us once the prologue's row offsets use the wave-uniform set
+// s_setprio of the MFMA waves in the loader-wave layers (0 = default arbitration)
+#ifndef CONV_MFMA_PRIO
+#define CONV_MFMA_PRIO 0
+#endif
 #ifndef CONV_DOWN2_PM
 #define CONV_DOWN2_PM 1
 #endif
@@ -1287,6 +1291,9 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
       st_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
       auto mainloop = [&](auto pat_tag) {
+#if CONV_MFMA_PRIO
+        __builtin_amdgcn_s_setprio(CONV_MFMA_PRIO);   // MFMA waves win issue over the loader wave on their SIMD
+#endif
         int buf = 0;
         for (int kc = 0; kc < NC; ++kc) {
           compute(smem + buf * G::STAGE, No{}, 0, 0, Seg1{}, 0, pat_tag);
