@@ -57,6 +57,11 @@
 #endif
 // down2 position-major (its 4 fragment sets keep 16/16/16/15 of 18): bitwise equal to sample-major;
 // down2 18.40 vs 18.64 us once the prologue's row offsets use the wave-uniform set
+// loader-wave layers: issue chunks 0, 1, 2 together at kernel start (0 = chunk 0 first, then 1 and 2
+// after it landed)
+#ifndef CONV_LDR_EARLY
+#define CONV_LDR_EARLY 0
+#endif
 // s_setprio of the MFMA waves in the loader-wave layers (0 = default arbitration)
 #ifndef CONV_MFMA_PRIO
 #define CONV_MFMA_PRIO 0
@@ -1274,10 +1279,22 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
     // Loader waves: chunk c lands in stage c % 3; barrier B(c+1) closes the MFMA waves'
     // work on chunk c, after which stage c % 3 takes chunk c + 3.
     if (loader) {
+#if CONV_LDR_EARLY
+      // all three stages are free at kernel start: chunks 1 and 2 go out right behind chunk 0,
+      // and B0 waits (counted vmcnt) for chunk 0's pieces only
+      static_assert(2 * G::PER < 64, "vmcnt range");
+      dma.all(smem, 0, 0, lane);
+      if (NC > 1) dma.all(smem, 1, 1, lane);
+      if (NC > 2) dma.all(smem, 2, 2, lane);
+      if (NC > 2) ring_barrier<2 * G::PER>();              // B0: chunk 0 landed
+      else if (NC > 1) ring_barrier<G::PER>();
+      else ring_barrier<0>();
+#else
       dma.all(smem, 0, 0, lane);
       ring_barrier<0>();                                   // B0: chunk 0 landed
       if (NC > 1) dma.all(smem, 1, 1, lane);
       if (NC > 2) dma.all(smem, 2, 2, lane);
+#endif
       for (int kc = 0; kc < NC; ++kc) {
         if (kc + 2 < NC) ring_barrier<G::PER>();           // chunk kc+1 landed, kc+2 in flight
         else ring_barrier<0>();
