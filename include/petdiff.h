@@ -175,6 +175,20 @@ int petdiff_philox_normal(petdiff_handle h, uint64_t seed, uint64_t sample_offse
 int petdiff_posterior_stats(petdiff_handle h, const float* x0_dev, const int32_t* tac_dev, int B, int n_tac,
                             double* stats_host, void* stream);
 
+/* Level outputs of the last petdiff_forward / petdiff_p_sample call, converted to
+ * fp32 into out_dev (test and debugging aid: per-level parity of the 16-bit fused
+ * path against the exact-f32 path and the oracle).  level (networks.py:1010-1072):
+ *   0 skip s0 = down0 ConvBlock output   [B][48][128]
+ *   1 skip s1 = down1 ConvBlock output   [B][24][256]
+ *   2 skip s2 = down2 ConvBlock output   [B][12][512]
+ *   3 down3 ConvBlock output (bottom)    [B][6][1024]
+ *   4 up0 ConvBlock output               [B][12][512]
+ *   5 up1 ConvBlock output               [B][24][256]
+ * (the up2 ConvBlock output stays in LDS: it feeds the fused final conv).  B must
+ * not exceed the batch of that call. */
+#define PETDIFF_NUM_LEVELS 6
+int petdiff_get_activation(petdiff_handle h, int level, float* out_dev, int B, void* stream);
+
 /* Per-layer kernel timing with HIP events on the launch stream (eager mode
  * only).  layer ids: 0 down0, 1..9 = down1, down2, down3, up0.conv2, up0.block,
  * up1.conv2, up1.block, up2.conv2, up2.block(+final+p_sample). */

@@ -7,8 +7,7 @@
  *   ImprovedDDPM.train_step          diffusion_model.py:533-598
  *                                    -> pettrain_step (= pettrain_compute_gradients
  *                                       + pettrain_apply_gradients)
- *   ImprovedDDPM.test_step           diffusion_model.py:600-640 -> pettrain_compute_gradients
- *                                       with update = 0 (loss only)
+ *   ImprovedDDPM.test_step           diffusion_model.py:600-640 -> pettrain_compute_loss
  *   _vb_terms_bpd / normal_kl /      diffusion_model.py:498-531, networks.py:29-80
  *   discretized_gaussian_log_likelihood
  *   compile(Adam(ExponentialDecay,   main_script.py:169-192, 233-234
@@ -76,6 +75,11 @@ void pettrain_destroy(pettrain_handle h);
 int pettrain_compute_gradients(pettrain_handle h, const float* x0_dev, const float* cond_dev, int B,
                                const int32_t* t_dev, const float* noise_dev, uint64_t seed,
                                uint64_t sample_offset, float* loss_dev, void* stream);
+/* Forward + loss only (ImprovedDDPM.test_step, diffusion_model.py:600-640): same draws and
+ * outputs as pettrain_compute_gradients, no backward pass; the gradient blob is untouched. */
+int pettrain_compute_loss(pettrain_handle h, const float* x0_dev, const float* cond_dev, int B, const int32_t* t_dev,
+                          const float* noise_dev, uint64_t seed, uint64_t sample_offset, float* loss_dev,
+                          void* stream);
 /* Clip (per variable, after scaling by grad_scale) + Adam update; iterations += 1. */
 int pettrain_apply_gradients(pettrain_handle h, float grad_scale, void* stream);
 /* compute_gradients + apply_gradients(1). */

@@ -206,7 +206,7 @@ def sinusoidal_pos_emb(t, dim=64, max_positions=10000., dt=F32):
 # --------------------------------------------------------------------------
 
 
-def unet_forward(P, x, t, cond, dt=np.float64, depth=4):
+def unet_forward(P, x, t, cond, dt=np.float64, depth=4, levels=None):
     """UnetConditional.call (networks.py:994-1093), shipped config.
 
     x (B,48,2), t (B,) int, cond (B,49,54) -> (B,48,n_out).
@@ -215,6 +215,7 @@ def unet_forward(P, x, t, cond, dt=np.float64, depth=4):
     saved before MaxPool (:1027).  Up level u (:1033-1072): concat
     [label | time | x] at the COARSE length, UpSampling, Conv1D(k=pool) (no
     activation), concat [skip | x] (:1057), ConvBlock.  Final Conv1D 1x1 (:1074).
+    ``levels`` (a dict) receives every ConvBlock output: 'down0'..'down3', 'up0'..'up2'.
     """
     P = {k: np.asarray(v, dtype=dt) for k, v in P.items()}
     x = np.asarray(x, dtype=dt)
@@ -245,6 +246,8 @@ def unet_forward(P, x, t, cond, dt=np.float64, depth=4):
         h = relu(conv1d_same(h, P[f'down{d}.conv.kernel'], P[f'down{d}.conv.bias']) +
                  conv1d_same(h, P[f'down{d}.res.kernel'], P[f'down{d}.res.bias']))
         skips.append(h)
+        if levels is not None:
+            levels[f'down{d}'] = h
         if d < depth - 1:
             h = maxpool2(h)
     for u in range(depth - 1):
@@ -255,6 +258,8 @@ def unet_forward(P, x, t, cond, dt=np.float64, depth=4):
         h = np.concatenate([skips[depth - 2 - u], h], axis=-1)
         h = relu(conv1d_same(h, P[f'up{u}.conv.kernel'], P[f'up{u}.conv.bias']) +
                  conv1d_same(h, P[f'up{u}.res.kernel'], P[f'up{u}.res.bias']))
+        if levels is not None:
+            levels[f'up{u}'] = h
     return conv1d_same(h, P['final.kernel'], P['final.bias'])
 
 

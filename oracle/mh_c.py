@@ -21,7 +21,8 @@ _D = C.POINTER(C.c_double)
 def lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(_HERE, 'lib', 'libmhref.so')
+        # MHREF_LIB: an alternative build of the same checker (scripts/asan_check.sh: AddressSanitizer)
+        path = os.environ.get('MHREF_LIB') or os.path.join(_HERE, 'lib', 'libmhref.so')
         if not os.path.exists(path):
             raise FileNotFoundError(f'{path} missing: run make -C oracle')
         L = C.CDLL(path)

@@ -21,6 +21,9 @@ PARAM_EPS, PARAM_X0, PARAM_V, PARAM_XPREV = 0, 1, 2, 3
 NTAB = 13
 MAX_BATCH = 65536                    # PETDIFF_MAX_BATCH (include/petdiff.h)
 NUM_LAYERS = 10
+NUM_LEVELS = 6                       # PETDIFF_NUM_LEVELS: petdiff_get_activation levels
+LEVEL_SHAPES = [(48, 128), (24, 256), (12, 512), (6, 1024), (12, 512), (24, 256)]
+LEVEL_NAMES = ['down0', 'down1', 'down2', 'down3', 'up0', 'up1']
 LAYER_NAMES = ['down0', 'down1', 'down2', 'down3', 'up0.conv2', 'up0.block', 'up1.conv2',
                'up1.block', 'up2.conv2', 'up2.block+final+p_sample']
 
@@ -54,6 +57,7 @@ SYMBOLS = [
                                           C.c_void_p]),
     ('petdiff_philox_normal', C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_int, C.c_void_p, C.c_int,
                                         C.c_void_p]),
+    ('petdiff_get_activation', C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p]),
     ('petdiff_set_timing', C.c_int, [C.c_void_p, C.c_int]),
     ('petdiff_get_timing', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ('petdiff_last_error', C.c_char_p, []),
@@ -94,6 +98,8 @@ SYMBOLS += [
     ('pettrain_destroy', None, [C.c_void_p]),
     ('pettrain_compute_gradients', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                              C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]),
+    ('pettrain_compute_loss', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                        C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]),
     ('pettrain_apply_gradients', C.c_int, [C.c_void_p, C.c_float, C.c_void_p]),
     ('pettrain_step', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64,
                                 C.c_uint64, C.c_void_p, C.c_void_p]),

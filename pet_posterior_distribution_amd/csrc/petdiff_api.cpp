@@ -146,6 +146,7 @@ struct petdiff_ctx {
   DevBuf enc_a, enc_b;               // encoder scratch
   // workspace
   int B_cap = 0;
+  int last_B = 0;                    // batch of the last forward / p_sample (petdiff_get_activation)
   DevBuf s0, p0, s1, p1, s2, p2, d3, u0, b0, u1, b1, u2;
   DevBuf s0b;                        // second s0 buffer (fused next-step down0 writes it)
   // run the next step's down0 inside the previous step's up2.block epilogue (generate);
@@ -754,7 +755,9 @@ int petdiff_forward(petdiff_handle h, const float* x, const int32_t* t, const in
   io.fin = base_final(h);
   io.fin.x_t = x;
   io.fin.net_out = out;
-  return network(h, io, B, (hipStream_t)stream);
+  CHK(network(h, io, B, (hipStream_t)stream));
+  h->last_B = B;
+  return PETDIFF_OK;
 }
 
 int petdiff_p_sample(petdiff_handle h, const float* x, const int32_t* t, const int32_t* tac, const float* z,
@@ -765,8 +768,7 @@ int petdiff_p_sample(petdiff_handle h, const float* x, const int32_t* t, const i
   if (B == 0) return PETDIFF_OK;
   CHK(ensure_workspace(h, B));
   hipStream_t s = (hipStream_t)stream;
-  const unsigned long long rp[2] = {seed, sample_offset};
-  HIPC(hipMemcpyAsync(h->rng.p, rp, 16, hipMemcpyHostToDevice, s));
+  HIPC(launch_set_rng(h->rng.as<unsigned long long>(), seed, sample_offset, 0, 1, s));
   StepIO io{};
   io.x_in = x;
   io.t_uniform = -1;
@@ -780,7 +782,7 @@ int petdiff_p_sample(petdiff_handle h, const float* x, const int32_t* t, const i
   io.fin.var_out = var;
   io.fin.var_tilde_out = var_tilde;
   CHK(network(h, io, B, s));
-  HIPC(hipStreamSynchronize(s));   // rp lives on this stack frame
+  h->last_B = B;
   return PETDIFF_OK;
 }
 
@@ -802,12 +804,9 @@ int petdiff_generate(petdiff_handle h, const float* x_T, const int32_t* tac, con
   const int parts = (graph && h->split > 1 && B >= 64) ? h->split : 1;
   int pb[kMaxSplit + 1];
   for (int k = 0; k <= parts; ++k) pb[k] = k == parts ? B : (int)((long long)B * k / parts / 32 * 32);
-  static thread_local unsigned long long rp[2 * kMaxSplit];
-  for (int k = 0; k < parts; ++k) {
-    rp[2 * k] = seed;
-    rp[2 * k + 1] = sample_offset + (unsigned long long)pb[k];
-  }
-  HIPC(hipMemcpyAsync(h->rng.p, rp, 16 * parts, hipMemcpyHostToDevice, s));
+  static_assert(kMaxSplit == 2, "set_rng_kernel writes at most two pairs");
+  HIPC(launch_set_rng(h->rng.as<unsigned long long>(), seed, sample_offset,
+                      sample_offset + (unsigned long long)pb[parts > 1 ? 1 : 0], parts, s));
   HIPC(hipMemcpyAsync(h->xa.p, x_T, xbytes, hipMemcpyDeviceToDevice, s));
   const int* tacp = nullptr;
   if (tac) {
@@ -901,6 +900,22 @@ int petdiff_posterior_stats(petdiff_handle h, const float* x0, const int32_t* ta
   HIPC(launch_posterior_stats(x0, tac, B, n_tac, ncol, d.as<double>(), s));
   HIPC(hipMemcpyAsync(stats, d.p, (size_t)n_tac * ncol * 3 * 8, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
+  return PETDIFF_OK;
+}
+
+int petdiff_get_activation(petdiff_handle h, int level, float* out, int B, void* stream) {
+  CHK(valid_handle(h));
+  if (level < 0 || level >= PETDIFF_NUM_LEVELS) return fail(PETDIFF_ERR_INVALID, "level out of range");
+  if (B < 0 || (B > 0 && !out)) return fail(PETDIFF_ERR_INVALID, "bad arguments");
+  if (B > h->last_B) return fail(PETDIFF_ERR_INVALID, "B exceeds the batch of the last forward / p_sample");
+  const DevBuf* bufs[PETDIFF_NUM_LEVELS] = {&h->s0, &h->s1, &h->s2, &h->d3, &h->b0, &h->b1};
+  const size_t per[PETDIFF_NUM_LEVELS] = {48 * 128, 24 * 256, 12 * 512, 6 * 1024, 12 * 512, 24 * 256};
+  const size_t n = (size_t)B * per[level];
+  hipStream_t s = (hipStream_t)stream;
+  const void* src = bufs[level]->p;
+  if (h->cfg.dtype == PETDIFF_DTYPE_BF16) HIPC(launch_to_f32<bf16>(static_cast<const bf16*>(src), n, out, s));
+  else if (h->cfg.dtype == PETDIFF_DTYPE_F16) HIPC(launch_to_f32<f16>(static_cast<const f16*>(src), n, out, s));
+  else HIPC(launch_to_f32<float>(static_cast<const float*>(src), n, out, s));
   return PETDIFF_OK;
 }
 

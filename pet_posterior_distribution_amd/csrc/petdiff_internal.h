@@ -91,6 +91,11 @@ hipError_t launch_conv(int layer_kind, const ConvArgs<T>& a, hipStream_t s);
 template <typename T>
 hipError_t launch_down0(const Down0Args& a, hipStream_t s);
 
+hipError_t launch_set_rng(unsigned long long* dst, unsigned long long seed, unsigned long long off0,
+                          unsigned long long off1, int parts, hipStream_t s);
+template <typename T>
+hipError_t launch_to_f32(const T* src, size_t n, float* dst, hipStream_t s);
+
 hipError_t launch_time_emb(const float* w, const float* b, int T, int sin_dim, int hid, float* out,
                            hipStream_t s);
 hipError_t launch_dense(const float* in, int rows, int din, const float* w, const float* b, int dout,

@@ -104,7 +104,8 @@ struct pettrain_ctx {
   Buf dy4, dA, dpre, d_out_up[3], d_out_dn3, d_pool[3], dskip[3], dhu, dlab, dtim, dz, dh_t, da_t, de1, de2, de3,
       sse, vlb, dbias_part, stats;
   int64_t iter = 0;
-  int last_B = 0;
+  int last_B = 0;          // batch of the last backward pass (gradients valid)
+  bool has_stats = false;  // a forward + loss ran (pettrain_last_stats valid)
 
   float* W(const std::string& n) const { return w.f() + off.at(n); }
   float* G(const std::string& n) const { return g.f() + off.at(n); }
@@ -252,7 +253,8 @@ int cond_bwd(pettrain_ctx* h, int p, int B, bool first) {
 }
 
 int forward_backward(pettrain_ctx* h, const float* x0, const float* cond, int B, const int32_t* t_in,
-                     const float* noise_in, uint64_t seed, uint64_t goff, float* loss_out, hipStream_t s) {
+                     const float* noise_in, uint64_t seed, uint64_t goff, float* loss_out, hipStream_t s,
+                     bool backward = true) {
   CHK(ensure(h, B));
   RBC(rocblas_set_stream(h->rb, s));
   const int R = B * 49;
@@ -321,7 +323,9 @@ int forward_backward(pettrain_ctx* h, const float* x0, const float* cond, int B,
   la.dbias_part = h->dbias_part.f();
   HIPC(K::loss(la, s));
   HIPC(K::loss_finish(h->sse.f(), h->vlb.f(), h->dbias_part.f(), B, n_out, B * 96, loss_out,
-                      reinterpret_cast<double*>(h->stats.p), h->G("final.bias"), s));
+                      reinterpret_cast<double*>(h->stats.p), backward ? h->G("final.bias") : nullptr, s));
+  h->has_stats = true;
+  if (!backward) return PETDIFF_OK;   // test_step: loss only, the gradient blob is untouched
 
   // ---------------- backward ----------------
   CHK(gemm(h, true, false, 128, n_out, B * 48, h->out_up[2].f(), 128, h->dy4.f(), n_out, h->G("final.kernel"), n_out,
@@ -476,6 +480,16 @@ int pettrain_compute_gradients(pettrain_handle h, const float* x0_dev, const flo
                           (hipStream_t)stream);
 }
 
+int pettrain_compute_loss(pettrain_handle h, const float* x0_dev, const float* cond_dev, int B, const int32_t* t_dev,
+                          const float* noise_dev, uint64_t seed, uint64_t sample_offset, float* loss_dev,
+                          void* stream) {
+  if (!h) return fail(PETDIFF_ERR_INVALID, "null handle");
+  if (B <= 0 || !x0_dev || !cond_dev) return fail(PETDIFF_ERR_INVALID, "bad arguments");
+  HIPC(hipSetDevice(h->device));
+  return forward_backward(h, x0_dev, cond_dev, B, t_dev, noise_dev, seed, sample_offset, loss_dev,
+                          (hipStream_t)stream, false);
+}
+
 int pettrain_apply_gradients(pettrain_handle h, float grad_scale, void* stream) {
   if (!h) return fail(PETDIFF_ERR_INVALID, "null handle");
   if (h->last_B <= 0) return fail(PETDIFF_ERR_INVALID, "no gradients computed yet");
@@ -538,7 +552,7 @@ int pettrain_get_weights(pettrain_handle h, float* dst_dev, void* stream) {
 
 int pettrain_last_stats(pettrain_handle h, double* out3, void* stream) {
   if (!h || !out3) return fail(PETDIFF_ERR_INVALID, "bad arguments");
-  if (h->last_B <= 0) return fail(PETDIFF_ERR_INVALID, "no step run yet");
+  if (!h->has_stats) return fail(PETDIFF_ERR_INVALID, "no step run yet");
   HIPC(hipMemcpyAsync(out3, h->stats.p, 3 * sizeof(double), hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIPC(hipStreamSynchronize((hipStream_t)stream));
   return PETDIFF_OK;

@@ -413,7 +413,7 @@ __global__ void loss_finish_kernel(const float* sse, const float* vlb, const flo
       if (threadIdx.x < o) s_sse[threadIdx.x] += s_sse[threadIdx.x + o];
       __syncthreads();
     }
-    if (threadIdx.x == 0) dbias[q] = (float)s_sse[0];
+    if (threadIdx.x == 0 && dbias) dbias[q] = (float)s_sse[0];   // null: loss-only pass
   }
   if (threadIdx.x == 0) {
     stats[0] = mse + s_vlb[0] / B;

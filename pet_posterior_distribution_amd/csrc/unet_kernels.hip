@@ -1920,6 +1920,25 @@ __global__ void posterior_stats_kernel(const float* x0, const int* tac, int B, i
   }
 }
 
+// {seed, sample_offset + start_k} pairs of the counter-based noise stream (FinalArgs::rng), written
+// on the stream from kernel arguments: no host buffer has to outlive the call (graph replays
+// read the pairs from device memory, so a cached graph serves every seed)
+__global__ void set_rng_kernel(unsigned long long* dst, unsigned long long seed, unsigned long long off0,
+                               unsigned long long off1, int parts) {
+  const int k = threadIdx.x;
+  if (k < parts) {
+    dst[2 * k] = seed;
+    dst[2 * k + 1] = k == 0 ? off0 : off1;
+  }
+}
+
+// 16-bit (or f32) activation buffer -> fp32 (petdiff_get_activation, level parity tests)
+template <typename T>
+__global__ void to_f32_kernel(const T* src, size_t n, float* dst) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = to_f(src[i]);
+}
+
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
@@ -1970,6 +1989,21 @@ hipError_t launch_down0(const Down0Args& a, hipStream_t s) {
 template hipError_t launch_conv<bf16>(int, const ConvArgs<bf16>&, hipStream_t);
 template hipError_t launch_conv<f16>(int, const ConvArgs<f16>&, hipStream_t);
 template hipError_t launch_conv<float>(int, const ConvArgs<float>&, hipStream_t);
+hipError_t launch_set_rng(unsigned long long* dst, unsigned long long seed, unsigned long long off0,
+                          unsigned long long off1, int parts, hipStream_t s) {
+  hipLaunchKernelGGL(set_rng_kernel, dim3(1), dim3(64), 0, s, dst, seed, off0, off1, parts);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_to_f32(const T* src, size_t n, float* dst, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(to_f32_kernel<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, n, dst);
+  return hipGetLastError();
+}
+template hipError_t launch_to_f32<bf16>(const bf16*, size_t, float*, hipStream_t);
+template hipError_t launch_to_f32<f16>(const f16*, size_t, float*, hipStream_t);
+template hipError_t launch_to_f32<float>(const float*, size_t, float*, hipStream_t);
 template hipError_t launch_down0<bf16>(const Down0Args&, hipStream_t);
 template hipError_t launch_down0<f16>(const Down0Args&, hipStream_t);
 template hipError_t launch_down0<float>(const Down0Args&, hipStream_t);

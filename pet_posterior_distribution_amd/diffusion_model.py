@@ -38,6 +38,26 @@ from .helper_func import NP_DTYPE, get_beta_schedule
 DTYPE = 'float32'   # dtype of every host-side table and of x (diffusion_model.py:7)
 
 
+_M64 = (1 << 64) - 1
+# noise-stream kinds of the automatically derived seeds (seed=None): p_sample calls, reverse loops
+# and test_step draws each get their own Philox key, so no two calls replay each other's noise
+STREAM_P_SAMPLE, STREAM_LOOP, STREAM_EVAL = 1, 2, 3
+
+
+def _mix64(x):
+    """splitmix64 finaliser (a bijection of 64-bit words)."""
+    x = (x + 0x9E3779B97F4A7C15) & _M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & _M64
+    return x ^ (x >> 31)
+
+
+def stream_seed(seed, kind, counter=0):
+    """Philox key of call ``counter`` of stream ``kind`` under the model seed (distinct model seeds,
+    kinds and counters give unrelated keys, unlike seed + counter)."""
+    return _mix64(_mix64((int(seed) & _M64) ^ (kind << 56)) ^ (int(counter) & _M64))
+
+
 def _as_device(x, device, dtype):
     if isinstance(x, torch.Tensor):
         return x.to(device=device, dtype=dtype).contiguous()
@@ -124,6 +144,7 @@ class ImprovedDDPM:
         self.device = torch.device('cuda', device if isinstance(device, int) else torch.device(device).index or 0)
         self.seed = int(seed)
         self._call_counter = 0
+        self._last_forward_B = 0
         self._handle = None
         self._cond_cache = None     # (unique-conditions tensor) last sent to the library
         self._trainer = None
@@ -191,6 +212,7 @@ class ImprovedDDPM:
         self.lambda_vlb_loss_tracker = _Mean('lambda_vlb_loss')
         self._trainer = None
         self._train_seed = self.seed
+        self._eval_calls = 0
 
     @property
     def metrics(self):
@@ -236,7 +258,12 @@ class ImprovedDDPM:
         if nz is not None and nz.shape != x0.shape:
             raise ValueError('noise must have the shape of images')
         loss = torch.empty(B, dtype=torch.float32, device=self.device)
-        tr.compute_gradients(x0, cond, tt, nz, seed=self._train_seed, loss=loss)
+        if update:
+            tr.compute_gradients(x0, cond, tt, nz, seed=self._train_seed, loss=loss)
+        else:
+            tr.compute_loss(x0, cond, tt, nz, seed=stream_seed(self._train_seed, STREAM_EVAL),
+                            sample_offset=self._eval_calls << 32, loss=loss)
+            self._eval_calls += 1
         if update:
             tr.apply_gradients(1.0)
             self._weights_stale = True
@@ -254,7 +281,9 @@ class ImprovedDDPM:
         return self._train_batch(data, t, noise, update=True)
 
     def test_step(self, data, t=None, noise=None):
-        """ImprovedDDPM.test_step (diffusion_model.py:600-640): loss only."""
+        """ImprovedDDPM.test_step (diffusion_model.py:600-640): loss only (no backward pass), with
+        fresh draws per call like the reference's tf.random: its own stream (STREAM_EVAL), and call k
+        at sample offset k * 2^32."""
         return self._train_batch(data, t, noise, update=False)
 
     def fit(self, x=None, y=None, batch_size=32, epochs=1, validation_split=0.0, shuffle=True, verbose=0,
@@ -341,7 +370,8 @@ class ImprovedDDPM:
                 not torch.equal(self._cond_cache, uniq):
             _lib.check(_lib.lib().petdiff_set_conditions(h, _ptr(uniq), uniq.shape[0], _stream_ptr(self.device)),
                        'petdiff_set_conditions')
-            self._cond_cache = uniq
+            # a private copy: the caller may update its condition buffer in place between calls
+            self._cond_cache = uniq.clone()
         return inv, uniq.shape[0]
 
     def _time(self, time, B):
@@ -364,6 +394,7 @@ class ImprovedDDPM:
         out = torch.empty((B, x.shape[1], self.network.n_out), dtype=torch.float32, device=self.device)
         _lib.check(_lib.lib().petdiff_forward(self._handle, _ptr(x), _ptr(t), _ptr(tac), _ptr(out), B,
                                               _stream_ptr(self.device)), 'petdiff_forward')
+        self._last_forward_B = B
         return out
 
     __call__ = call
@@ -377,19 +408,35 @@ class ImprovedDDPM:
         zt = None if z is None else _as_device(z, self.device, torch.float32)
         if zt is not None and zt.shape != x.shape:
             raise ValueError('z must have the shape of x_t')
+        if seed is None:
+            seed = stream_seed(self.seed, STREAM_P_SAMPLE)
         if rng_step is None:
-            rng_step = self._call_counter
+            rng_step = self._call_counter & 0x7FFFFFFF
             self._call_counter += 1
         mean = torch.empty_like(x)
         var = torch.empty_like(x)
         var_tilde = torch.empty_like(x)
         _lib.check(_lib.lib().petdiff_p_sample(
-            self._handle, _ptr(x), _ptr(t), _ptr(tac), _ptr(zt), self.seed if seed is None else int(seed),
+            self._handle, _ptr(x), _ptr(t), _ptr(tac), _ptr(zt), int(seed),
             int(sample_offset), int(rng_step), _ptr(mean), _ptr(var), _ptr(var_tilde), B,
             _stream_ptr(self.device)), 'petdiff_p_sample')
+        self._last_forward_B = B
         return mean, var, var_tilde
 
     p_sample = ddpm
+
+    def level_outputs(self, B=None):
+        """fp32 copies of the per-level ConvBlock outputs of the last call / ddpm (networks.py:1010-1072):
+        {'down0': (B, 48, 128), ..., 'down3': (B, 6, 1024), 'up0': (B, 12, 512), 'up1': (B, 24, 256)}."""
+        h = self._ensure_handle()
+        out = {}
+        for lv, (name, (L, C_)) in enumerate(zip(_lib.LEVEL_NAMES, _lib.LEVEL_SHAPES)):
+            n = B if B is not None else self._last_forward_B
+            buf = torch.empty((n, L, C_), dtype=torch.float32, device=self.device)
+            _lib.check(_lib.lib().petdiff_get_activation(h, lv, _ptr(buf), n, _stream_ptr(self.device)),
+                       'petdiff_get_activation')
+            out[name] = buf
+        return out
 
     def tfunc_ddpm(self, x_t, time, condition=None, **kwargs):
         """diffusion_model.py:665-668."""
@@ -428,7 +475,7 @@ class ImprovedDDPM:
         out = torch.empty_like(x)
         tseq = np.ascontiguousarray(np.asarray(indices, dtype=np.int32))
         if seed is None:
-            seed = self.seed + self._call_counter
+            seed = stream_seed(self.seed, STREAM_LOOP, self._call_counter)
             self._call_counter += 1
         # batches above PETDIFF_MAX_BATCH run as chunks (main_script.py:414-427 chunks the same way);
         # sample b of chunk c is global sample sample_offset + c0 + b, so the noise is unchanged
@@ -456,7 +503,15 @@ class ImprovedDDPM:
     generate = ddpm_loop
 
     def tfunc_ddpm_loop(self, x_T, condition, **kwargs):
-        """diffusion_model.py:718-737: full-T loop, var_tilde, one captured graph."""
+        """diffusion_model.py:718-737: full-T loop, var_tilde, one captured graph.
+
+        Unlike ddpm_loop (:697-699), the reference passes ``condition`` to the network unchanged
+        (no tf.repeat), so its batch must equal x_T's; a mismatch raises ValueError here."""
+        B = int(x_T.shape[0])
+        cb = 1 if np.ndim(condition) == 2 else int(condition.shape[0])
+        if cb != B:
+            raise ValueError(f'tfunc_ddpm_loop: condition batch {cb} != x_T batch {B} '
+                             '(the reference does not broadcast the condition here)')
         return self.ddpm_loop(x_T, condition, num_timesteps=None, flag_var_tilde=True, use_graph=True, **kwargs)
 
     def philox_normal(self, B, seed=None, sample_offset=0, rng_step=0x7fffffff):

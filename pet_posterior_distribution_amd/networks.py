@@ -87,7 +87,7 @@ def glorot_uniform_init(spec, seed=1234, bias_scale=0.0, final_scale=1.0):
     return out
 
 
-def denoiser_init(spec, seed=1234, perturb=0.1, bias_scale=0.0):
+def denoiser_init(spec, seed=1234, perturb=0.1, bias_scale=0.0, v_perturb=None):
     """Synthetic weights that behave like a trained eps-predictor (bounded 1000-step chain).
 
     An untrained Glorot net predicts eps ~ 0, and at t = 999 the eps
@@ -98,6 +98,8 @@ def denoiser_init(spec, seed=1234, perturb=0.1, bias_scale=0.0):
     them from the skip, and the final 1x1 conv maps them back to eps = x.  All
     other final-conv rows are scaled by ``perturb`` so the rest of the network
     (condition, time, all levels) perturbs eps and v by a small amount.
+    ``v_perturb`` (learned variance): scale of the v output rows instead of ``perturb``
+    (1.0 = the full Glorot network drives the log-variance interpolation).
     """
     w = glorot_uniform_init(spec, seed=seed, bias_scale=bias_scale)
     names = dict(spec)
@@ -123,7 +125,11 @@ def denoiser_init(spec, seed=1234, perturb=0.1, bias_scale=0.0):
     for c in range(2 * n_par):
         k[ctr, c, c] = 1.0
     f = w['final.kernel']
-    f *= perturb
+    if v_perturb is not None and n_out == 2 * n_par:
+        f[..., :n_par] *= perturb
+        f[..., n_par:] *= v_perturb
+    else:
+        f *= perturb
     f[0, :2 * n_par, :] = 0.0
     for p in range(n_par):
         f[0, 2 * p, p] = 1.0

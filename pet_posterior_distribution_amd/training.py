@@ -140,6 +140,13 @@ class Trainer:
         check(_lib.lib().pettrain_compute_gradients(self.handle, _p(x0), _p(cond), B, _p(t), _p(noise), int(seed),
                                                     int(sample_offset), _p(loss), st), 'pettrain_compute_gradients')
 
+    def compute_loss(self, x0, cond, t=None, noise=None, seed=0, sample_offset=0, loss=None):
+        """Forward + loss only (test_step): the gradient blob is left untouched."""
+        B = x0.shape[0]
+        st = _stream(self.device)
+        check(_lib.lib().pettrain_compute_loss(self.handle, _p(x0), _p(cond), B, _p(t), _p(noise), int(seed),
+                                               int(sample_offset), _p(loss), st), 'pettrain_compute_loss')
+
     def apply_gradients(self, grad_scale=1.0):
         st = _stream(self.device)
         check(_lib.lib().pettrain_apply_gradients(self.handle, float(grad_scale), st), 'pettrain_apply_gradients')

@@ -23,3 +23,45 @@ def mh_problem(g2, case=0, noise=0.1, seed=0):
     pr = synthetic_prior()
     return dict(time_vector=tv, tac_ref=ref, k2p=k2p, y_obs=y, sigma_noise=sig, mu_DVR=truth_D * 1.02,
                 Cov_DVR=pr['Cov_DVR'], mu_R1=truth_R * 0.98, Cov_R1=pr['Cov_R1'])
+
+
+_TRAINED = {}
+
+
+def quick_trained_weights(steps=800, seed=5, lr=2e-4):
+    """Weights of the shipped network after `steps` Adam steps (batch 256, lr 2e-4, clipnorm 1.5,
+    main_script.py:169-174) on GPU-simulated training data (sim_data.simulate_dataset, 16,384
+    samples): an eps-predictor whose 1000-step reverse chain stays bounded without any identity
+    shortcut, so the bf16 / f32 comparisons see the whole network.  About 3 s on one MI355X;
+    cached per process.  Returns (weights dict, one condition (49, 54) of the data set)."""
+    key = (steps, seed, lr)
+    if key in _TRAINED:
+        return _TRAINED[key]
+    import numpy as np
+    import torch
+    from pet_posterior_distribution_amd import ImprovedDDPM, UnetConditional, Adam
+    from pet_posterior_distribution_amd.networks import glorot_uniform_init
+    from pet_posterior_distribution_amd.sim_data import simulate_dataset
+    net = UnetConditional(**shipped_net_args())
+    net.build((None, 48, 2))
+    net.weights = glorot_uniform_init(net.spec(), seed=seed)
+    m = ImprovedDDPM(network=net, dtype='float32', **shipped_diff_args())
+    m.compile(optimizer=Adam(learning_rate=lr, clipnorm=1.5))
+    nb, B = 64, 256
+    d = simulate_dataset(nb * B, seed=3)
+    x0 = torch.stack([d['varDVR'], d['varR1']], -1).to(torch.float32).contiguous()
+    cond = d['condition']
+    tr = m._ensure_trainer()
+    for i in range(steps):
+        k = i % nb
+        tr.compute_gradients(x0[k * B:(k + 1) * B], cond[k * B:(k + 1) * B], seed=11)
+        tr.apply_gradients(1.0)
+    w = tr.weights().cpu().numpy()
+    out, o = {}, 0
+    for name, sh in net.spec():
+        k = int(np.prod(sh))
+        out[name] = w[o:o + k].reshape(sh).copy()
+        o += k
+    tr.close()
+    _TRAINED[key] = (out, cond[0].cpu().numpy())
+    return _TRAINED[key]

@@ -342,3 +342,16 @@ def test_bench_pmc_fields_known_answer():
     assert f['mfma_busy_vs_active'] == round(32 * n_mfma / (1024 * 100_000), 4)
     none = bench.pmc_fields({'traffic': None, 'mfma_busy': None, 'grbm': None, 'source': None}, 1e-4)
     assert none['hbm_gbs'] is None and none['mfma_util'] is None
+
+
+def test_default_noise_stream_keys_distinct():
+    """diffusion_model.stream_seed: the keys of default-seeded calls differ across call kinds,
+    counters and model seeds (the round-1 scheme seed + counter made model seed s at call c+1 reuse
+    model seed s+1 at call c, and loops reuse p_sample keys)."""
+    from pet_posterior_distribution_amd.diffusion_model import (stream_seed, STREAM_P_SAMPLE, STREAM_LOOP,
+                                                                STREAM_EVAL)
+    keys = {stream_seed(s, k, c) for s in range(4) for k in (STREAM_P_SAMPLE, STREAM_LOOP, STREAM_EVAL)
+            for c in range(50)}
+    assert len(keys) == 4 * 3 * 50
+    assert all(0 <= k < 2 ** 64 for k in keys)
+    assert stream_seed(12345, STREAM_LOOP, 0) not in (12345, 12346)

@@ -72,8 +72,9 @@ def test_mh_chain_path_matches_oracle(g2):
     res = mh.run(n_chains, draws, tune, seed=seed, return_chains=True)
 
     def logp(x):
-        return K.log_posterior(x[:48], x[48:], P['k2p'], P['y_obs'], P['sigma_noise'], P['time_vector'],
-                               P['tac_ref'], P['mu_DVR'], P['Cov_DVR'], P['mu_R1'], P['Cov_R1'])
+        with np.errstate(over='ignore', invalid='ignore'):   # DVR <= 0 proposals: test_mh_chain_rejects_...
+            return K.log_posterior(x[:48], x[48:], P['k2p'], P['y_obs'], P['sigma_noise'], P['time_vector'],
+                                   P['tac_ref'], P['mu_DVR'], P['Cov_DVR'], P['mu_R1'], P['Cov_R1'])
     x0 = np.concatenate([P['mu_DVR'], P['mu_R1']])
     for ch in range(n_chains):
         dr, acc = K.metropolis_elemwise_philox(logp, x0, draws, tune, seed, ch)
@@ -131,4 +132,71 @@ def test_mh_trace_matches_welford(g2):
     np.testing.assert_allclose(res['chain_stats'][..., 2], ((tr - tr.mean(1, keepdims=True)) ** 2).sum(1),
                                rtol=1e-9, atol=1e-14)
     np.testing.assert_array_equal(res['last'], tr[:, -1])
+    mh.close()
+
+
+def _same_class(a, b):
+    """Both finite and within 1e-10 relative, or the same non-finite value (nan / +inf / -inf)."""
+    if np.isfinite(a) and np.isfinite(b):
+        return abs(a - b) <= 1e-10 * abs(b)
+    return (np.isnan(a) and np.isnan(b)) or a == b
+
+
+def test_logp_edge_cases_vs_oracle(g2):
+    """Deliberate edge cases of the model (mcmc.py:147-155): DVR near 0 (SRTM2 TAC goes negative in
+    late frames -> the sn < 0 -> 1e-6 switch of :152), DVR = 0, DVR < 0 (exp(-k2a t) overflows: the
+    model TAC is +-inf / nan), R1 < 0.  GPU and oracle agree value for value, non-finite included."""
+    from pet_posterior_distribution_amd.mcmc import MetropolisSRTM2
+    P = make_problem(g2, case=1)
+    mh = MetropolisSRTM2(**P)
+    base = np.concatenate([P['mu_DVR'], P['mu_R1']])
+    pts, hit_clamp = [], False
+    for dvr in (0.03, 0.01, 0.0, -0.002, -0.05, -1.0):
+        p = base.copy()
+        p[[3, 17, 40]] = dvr
+        pts.append(p)
+        if dvr > 0:
+            sn = K.srtm2_tac(P['time_vector'], P['tac_ref'], p[:48], p[48:], P['k2p'])
+            hit_clamp |= bool((sn < 0).any())
+    p = base.copy()
+    p[48 + 5] = -0.3                                    # R1 < 0
+    pts.append(p)
+    assert hit_clamp, 'no point exercised the sn < 0 switch'
+    pts = np.stack(pts)
+    got = mh.logp(pts).cpu().numpy()
+    with np.errstate(all='ignore'):
+        ref = [K.log_posterior(q[:48], q[48:], P['k2p'], P['y_obs'], P['sigma_noise'], P['time_vector'],
+                               P['tac_ref'], P['mu_DVR'], P['Cov_DVR'], P['mu_R1'], P['Cov_R1']) for q in pts]
+    assert any(not np.isfinite(r) for r in ref), 'no point produced a non-finite density'
+    bad = [(k, got[k], ref[k]) for k in range(len(ref)) if not _same_class(got[k], ref[k])]
+    assert not bad, bad
+    mh.close()
+
+
+def test_mh_chain_rejects_nonfinite_proposals(g2):
+    """Chains started next to DVR = 0 with unit proposals: many proposals make the density
+    non-finite (DVR <= 0); metrop_select's isfinite rule rejects them.  The GPU chain path equals
+    the oracle's on the same Philox stream, and the oracle confirms such proposals occurred."""
+    from pet_posterior_distribution_amd.mcmc import MetropolisSRTM2
+    P = make_problem(g2, case=0)
+    mh = MetropolisSRTM2(**P)
+    x0 = np.concatenate([P['mu_DVR'], P['mu_R1']])
+    x0[:8] = 0.02
+    n_chains, draws, tune, seed = 2, 5, 3, 4242
+    res = mh.run(n_chains, draws, tune, seed=seed, x0=np.repeat(x0[None], n_chains, 0), return_chains=True)
+    n_bad = [0]
+
+    def logp(x):
+        with np.errstate(all='ignore'):
+            v = K.log_posterior(x[:48], x[48:], P['k2p'], P['y_obs'], P['sigma_noise'], P['time_vector'],
+                                P['tac_ref'], P['mu_DVR'], P['Cov_DVR'], P['mu_R1'], P['Cov_R1'])
+        n_bad[0] += not np.isfinite(v)
+        return v
+    for ch in range(n_chains):
+        dr, acc = K.metropolis_elemwise_philox(logp, x0, draws, tune, seed, ch)
+        assert np.isfinite(dr).all()
+        np.testing.assert_allclose(res['last'][ch], dr[-1], rtol=1e-9)
+        np.testing.assert_allclose(res['chain_stats'][ch][:, 1], dr.mean(0), rtol=1e-9, atol=1e-12)
+    assert n_bad[0] > 0
+    assert np.isfinite(res['last']).all()
     mh.close()

@@ -56,9 +56,16 @@ def test_loss_and_gradients_vs_oracle(lv, param):
     m = make(lv, param)
     P = {k: v.astype(np.float64) for k, v in m.network.weights.items()}
     x0, cond, t, noise = batch()
-    m.test_step((x0, cond), t=t, noise=noise)
+    m.test_step((x0, cond), t=t, noise=noise)             # loss only (no backward pass)
     loss = m.last_loss.cpu().numpy()
-    g = split(m._trainer.gradients().cpu().numpy(), m.network.spec())
+    tr = m._ensure_trainer()
+    dev = m.device
+    lg = torch.empty(x0.shape[0], dtype=torch.float32, device=dev)
+    tr.compute_gradients(torch.as_tensor(x0, device=dev), torch.as_tensor(cond, device=dev),
+                         torch.as_tensor(t, dtype=torch.int32, device=dev), torch.as_tensor(noise, device=dev),
+                         loss=lg)
+    np.testing.assert_array_equal(lg.cpu().numpy(), loss)   # test_step's forward = the training forward
+    g = split(tr.gradients().cpu().numpy(), m.network.spec())
     rl, mse, vlb, G = TR.train_loss_and_grads(P, S, x0, cond, t, noise, learn_variance=lv, parameterization=param)
     assert np.abs(loss - rl).max() <= 1e-4 * np.abs(rl).max()
     bad = {}
@@ -143,3 +150,24 @@ def test_sharded_draws_match_unsharded():
     full = l_full.cpu().numpy() - s1[1]
     tr_stats_b = tr.last_stats()
     np.testing.assert_allclose(l_b.cpu().numpy() - tr_stats_b[1], full[3:], rtol=1e-5, atol=1e-6)
+
+
+def test_test_step_fresh_draws_and_no_backward():
+    """test_step (diffusion_model.py:600-640) draws fresh t / noise per call like the reference's
+    tf.random (its own stream, never the training step's draws), runs no backward pass (the
+    gradient blob and the iteration count are untouched) and does not update the weights."""
+    x0, cond, t, noise = batch(B=16, seed=13)
+    m = make(lr=1e-3)
+    m.train_step((x0, cond), t=t, noise=noise)
+    tr = m._trainer
+    g0 = tr.gradients().cpu().numpy()
+    w0 = tr.weights().cpu().numpy()
+    it0 = tr.iterations
+    m.test_step((x0, cond))
+    l1 = m.last_loss.cpu().numpy().copy()
+    m.test_step((x0, cond))
+    l2 = m.last_loss.cpu().numpy().copy()
+    assert not np.array_equal(l1, l2)                         # fresh draws per call
+    np.testing.assert_array_equal(tr.gradients().cpu().numpy(), g0)
+    np.testing.assert_array_equal(tr.weights().cpu().numpy(), w0)
+    assert tr.iterations == it0
