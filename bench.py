@@ -40,6 +40,14 @@ PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0                       # HBM3E (MI355X_MICROARCH.md)
 PEAK_CLOCK_HZ = 2.4e9                       # engine clock the dense MFMA peak is quoted at
 N_SIMD = 256 * 4                            # 256 CUs x 4 SIMDs
+# FLOP the kernels EXECUTE per sample-step: the label / time input channels of every concat are
+# hoisted into per-level maps and the 1x1 residuals folded into the centre tap, so the convs multiply
+# only the x channels: down0 (VALU) + down1..3 + the up levels' k2 convs and blocks (unfused, as the
+# exact-f32 path runs them) + the final 1x1 conv
+EXEC_FLOP_PER_SAMPLE_STEP_UNFUSED = 2 * (48 * 6 * 2 * 128 + 24 * 6 * 128 * 256 + 12 * 6 * 256 * 512 +
+                                         6 * 6 * 512 * 1024 + 12 * 2 * 1024 * 512 + 12 * 6 * 1024 * 512 +
+                                         24 * 2 * 512 * 256 + 24 * 6 * 512 * 256 + 48 * 2 * 256 * 128 +
+                                         48 * 6 * 256 * 128 + 48 * 128 * 4)
 # training step: forward + data grad + weight grad of every layer, incl. the
 # per-sample condition encoder / label projections / time MLP (6,002,304 FLOP per sample forward)
 TRAIN_FLOP_PER_SAMPLE = 3 * (FLOP_PER_SAMPLE_STEP + 6_002_304)
@@ -61,6 +69,8 @@ def parse():
     ap.add_argument('--dtype', default='bfloat16', choices=['bfloat16', 'float16', 'float32'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-kernel-timing', action='store_true')
+    ap.add_argument('--no-extras', action='store_true',
+                    help='skip the exact-f32 rate, the MH configs[2] slice and the reference-protocol ratio')
     ap.add_argument('--workload', default='iddpm', choices=['iddpm', 'mh', 'train'],
                     help='iddpm: BASELINE configs[1] (the metric); mh: configs[2] MH/SRTM2 baseline')
     ap.add_argument('--train-batch', type=int, default=256, help='training batch per GPU (main_script.py:169)')
@@ -373,6 +383,81 @@ def main_train(args):
         dist.destroy_process_group()
 
 
+def f32_exact_rate(cond, B, n_rev, dev):
+    """The reference's own precision (diffusion_model.py:7-10, fp32): the same generate() on the
+    exact-f32 MFMA network (v_mfma_f32_32x32x2_f32; the path the 1e-4 parity tests run), one graph
+    warm-up + one timed run of B samples x n_rev steps."""
+    import torch
+    from pet_posterior_distribution_amd import ImprovedDDPM, UnetConditional
+    from pet_posterior_distribution_amd.configs import shipped_net_args, shipped_diff_args
+    net = UnetConditional(**shipped_net_args(), seed=1234)
+    net.build((None, 48, 2))
+    m = ImprovedDDPM(network=net, dtype='float32', device=dev.index, **shipped_diff_args())
+    x = m.philox_normal(B, seed=5)
+    m.ddpm_loop(x, cond[None], num_timesteps=n_rev, seed=2)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = m.ddpm_loop(x, cond[None], num_timesteps=n_rev, seed=2)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    tf = FLOP_PER_SAMPLE_STEP * n_rev * B / el / 1e12
+    te = EXEC_FLOP_PER_SAMPLE_STEP_UNFUSED * n_rev * B / el / 1e12
+    m.close()
+    return {'value': round(B / el, 2), 'unit': 'samples/s', 'dtype': 'f32', 'n_posterior': B,
+            'reverse_steps': n_rev, 'ms_per_generate': round(el * 1e3, 2),
+            'pipeline_tflops': round(tf, 2), 'peak': PEAK_F32_TFLOPS, 'frac': round(tf / PEAK_F32_TFLOPS, 4),
+            'executed_tflops': round(te, 2), 'executed_frac': round(te / PEAK_F32_TFLOPS, 4),
+            'finite': bool(torch.isfinite(out).all()),
+            'note': 'frac: algorithmic FLOP (SURVEY 8(d): every Conv1D incl. its label/time channels and 1x1 '
+                    'residual); the kernels hoist the label/time channels into maps and fold the residual into '
+                    'the centre tap, so they execute 0.82 of that (executed_frac) and frac can exceed 1'}
+
+
+def mh_slice_and_protocol(iddpm_10k_s, dev):
+    """BASELINE configs[2] slice (10k chains x 500 steps of the 20k) and the reference's per-TAC
+    MCMC protocol (main_script.py:363-364, pymc's default 4 chains: 4 x (20k draws + 40k tune)),
+    timed as a 1/10 slice x 10; ratio against iDDPM's 10,000 posterior samples of one TAC
+    (main_script.py:315-319) on the same GPU -- the README.md:12 '> 230x' claim, same silicon."""
+    import torch
+    from pet_posterior_distribution_amd.mcmc import MetropolisSRTM2
+    from pet_posterior_distribution_amd.sim_data import mh_problem
+    mh = MetropolisSRTM2(**mh_problem(seed=0))
+    mh.run(512, 2, 0, seed=1)
+    torch.cuda.synchronize()
+    n, tune, draws = 10000, 250, 250
+    t0 = time.perf_counter()
+    res = mh.run(n, draws, tune, seed=7)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    steps = n * (tune + draws)
+    fl = steps * 96 * MH_FP64_FLOP_PER_UPDATE / el / 1e12
+    t1 = time.perf_counter()
+    mh.run(4, 2000, 4000, seed=3)
+    torch.cuda.synchronize()
+    proto = (time.perf_counter() - t1) * 10
+    mh.close()
+    return ({'value': round(steps / el, 1), 'unit': 'chain-steps/s', 'chains': n, 'steps_per_chain': tune + draws,
+             'seconds': round(el, 3), 'fp64_tflops': round(fl, 2), 'frac': round(fl / 78.6, 4),
+             'mean_accept_rate': round(float(res['accept_rate'].mean()), 4)},
+            {'mh_protocol_s_per_tac': round(proto, 3), 'mh_protocol': '4 chains x (20000 draws + 40000 tune), '
+             'timed as 4 x (2000 + 4000) x 10', 'iddpm_s_per_tac': round(iddpm_10k_s, 3),
+             'iddpm_protocol': '10,000 posterior samples x 1000 reverse steps, bf16, one launch',
+             'iddpm_speedup_over_mh': round(proto / iddpm_10k_s, 2), 'reference_claim': '> 230x (README.md:12)'})
+
+
+def iddpm_10k_seconds(model, cond):
+    """One TAC's posterior as the reference draws it: n_posterior = chunk_size = 10,000 samples in one
+    ddpm_loop (main_script.py:315-319, 414-420), graph warm-up then one timed run."""
+    import torch
+    x = model.philox_normal(10000, seed=9)
+    model.ddpm_loop(x, cond[None], seed=4)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    model.ddpm_loop(x, cond[None], seed=4)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
 def main():
     args = parse()
     if args.workload == 'mh':
@@ -503,6 +588,10 @@ def main():
             line['cpu_baseline'] = cpu_baseline(net.weights, cond[0])
         else:
             line['cpu_baseline'] = None
+        if world == 1 and not args.no_extras and args.dtype == 'bfloat16' and n_rev == 1000 and n_tac == 1:
+            line['f32_exact'] = f32_exact_rate(cond[0], B, n_rev, dev)
+            t10k = iddpm_10k_seconds(model, cond[0])
+            line['mh_config3_slice'], line['reference_protocol'] = mh_slice_and_protocol(t10k, dev)
         sm = allst[..., 1]
         line['posterior_mean_DVR_roi0'] = [round(float(v), 5) for v in sm[:, 0, 0]]
         print(json.dumps(line), flush=True)
