@@ -28,6 +28,7 @@ sharded over GPUs.  ``z=`` injects explicit noise (used by the parity tests).
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 import torch
@@ -289,7 +290,19 @@ class ImprovedDDPM:
     def fit(self, x=None, y=None, batch_size=32, epochs=1, validation_split=0.0, shuffle=True, verbose=0,
             callbacks=None, **kwargs):
         """keras Model.fit as the reference calls it (main_script.py:267-271): per epoch, shuffled
-        batches through train_step, then test_step over the held-out validation tail."""
+        batches through train_step, then test_step over the held-out validation tail.  ``callbacks``
+        follow the Keras protocol the reference's WeightsCheckpoint uses (networks.py:152-180):
+        set_model / on_train_begin / on_epoch_end(epoch, logs) / on_train_end, and a callback may set
+        ``model.stop_training``.  ``verbose`` prints one line per epoch."""
+        callbacks = list(callbacks or [])
+        self.stop_training = False
+        for cb in callbacks:
+            if hasattr(cb, 'set_model'):
+                cb.set_model(self)
+            else:
+                cb.model = self
+            if hasattr(cb, 'on_train_begin'):
+                cb.on_train_begin({})
         x = np.asarray(x, dtype=np.float32) if not isinstance(x, torch.Tensor) else x
         y = np.asarray(y, dtype=np.float32) if not isinstance(y, torch.Tensor) else y
         n = x.shape[0]
@@ -301,7 +314,9 @@ class ImprovedDDPM:
         history = {m.name: [] for m in self.metrics}
         if n_val:
             history.update({'val_' + m.name: [] for m in self.metrics})
-        for _ in range(epochs):
+        for epoch in range(epochs):
+            if self.stop_training:
+                break
             for m in self.metrics:
                 m.reset_state()
             order = rng.permutation(n_tr) if shuffle else np.arange(n_tr)
@@ -317,11 +332,35 @@ class ImprovedDDPM:
                     self.test_step((xd[s:min(s + batch_size, n)], yd[s:min(s + batch_size, n)]))
                 for m in self.metrics:
                     history['val_' + m.name].append(m.result())
+            logs = {k: v[-1] for k, v in history.items()}
+            if verbose:
+                print(f'epoch {epoch + 1}/{epochs} ' + ' '.join(f'{k} {v:.5g}' for k, v in logs.items()),
+                      flush=True)
+            for cb in callbacks:
+                if hasattr(cb, 'on_epoch_end'):
+                    cb.on_epoch_end(epoch, logs)
+        for cb in callbacks:
+            if hasattr(cb, 'on_train_end'):
+                cb.on_train_end({})
         return history
 
-    def load_weights(self, path):
-        self.network.load_weights(path)
+    def load_weights(self, path, strict=True):
+        """diff_model.load_weights (main_script.py:412): the network's weights from an .npz, a SavedModel /
+        TensorBundle checkpoint or a Keras ``.weights.h5`` of this model (group ``network``)."""
+        self._sync_trained_weights()
+        self.network.load_weights(path, strict=strict)
+        self._trainer = None
         self.close()
+
+    def save_weights(self, path):
+        """model.save_weights as WeightsCheckpoint calls it (networks.py:176): ``.h5`` writes the Keras layout
+        with the network under ``network/`` (h5.save_unet_h5), anything else this package's .npz."""
+        self._sync_trained_weights()
+        if os.fspath(path).endswith('.h5'):
+            from .h5 import save_unet_h5
+            save_unet_h5(path, self.network.weights, network_path='network')
+        else:
+            self.network.save_weights(path)
 
     def close(self):
         if self._handle is not None:

@@ -230,15 +230,21 @@ class UnetConditional:
         return np.concatenate([self.weights[n].ravel() for n, _ in self.spec()]).astype(NP_DTYPE)
 
     def save_weights(self, path):
+        """``.npz`` (+ ``.json`` spec), or Keras-layout HDF5 when the path ends in ``.h5`` (h5.save_unet_h5)."""
+        if os.fspath(path).endswith('.h5'):
+            from .h5 import save_unet_h5
+            save_unet_h5(path, self.weights, network_path='')
+            return
         np.savez(path, **self.weights)
         with open(os.path.splitext(path)[0] + '.json', 'w') as f:
             json.dump({'spec': [[n, list(s)] for n, s in self.spec()]}, f)
 
-    def load_weights(self, path):
+    def load_weights(self, path, strict=True):
         """Weights from this package's .npz, or from a TensorFlow checkpoint of the reference: a SavedModel
         directory (`cp_<epoch>/`, main_script.py:263) or a TensorBundle prefix (`.../variables/variables`),
-        read by checkpoint.py without TensorFlow.  Keras `.weights.h5` files (main_script.py:412) need an HDF5
-        reader, which this environment lacks."""
+        read by checkpoint.py without TensorFlow, or a Keras `.weights.h5` file (main_script.py:412), read by
+        h5.py without h5py.  ``strict=False`` (h5 only) keeps the current value of every variable the file lacks
+        (Keras 3 does not store layers held in nested Python lists, see h5.unet_h5_paths)."""
         path = os.fspath(path)
         if path.endswith('.index'):
             path = path[:-len('.index')]
@@ -247,7 +253,11 @@ class UnetConditional:
             self.set_weights(load_unet_weights(path, self.spec()))
             return
         if path.endswith('.h5'):
-            raise NotImplementedError('Keras .weights.h5 (HDF5) is not readable here; pass the SavedModel '
-                                      'checkpoint directory (cp_<epoch>/) instead')
+            from .h5 import load_unet_h5
+            got = load_unet_h5(path, self.spec(), strict=strict)
+            if not strict and self.weights is not None:
+                got = {**self.weights, **got}
+            self.set_weights(got)
+            return
         with np.load(path, allow_pickle=False) as z:
             self.set_weights({n: z[n] for n, _ in self.spec()})

@@ -87,6 +87,34 @@ class _Mean:
         self.count = 0.0
 
 
+class WeightsCheckpoint:
+    """networks.WeightsCheckpoint (networks.py:152-180): every ``every_n_epochs`` epochs save the
+    model's weights to ``root_dir/cp_<epoch>/<filename>`` (this package's .npz + .json spec; the
+    reference's ``ckpt.weights.h5`` is Keras HDF5)."""
+
+    def __init__(self, root_dir, every_n_epochs=1, filename='ckpt.weights.npz', overwrite=True):
+        self.root_dir = root_dir
+        self.every_n_epochs = int(every_n_epochs)
+        self.filename = filename
+        self.overwrite = overwrite
+        self.model = None
+
+    def set_model(self, model):
+        self.model = model
+
+    def on_epoch_end(self, epoch, logs=None):
+        import os
+        if (epoch + 1) % self.every_n_epochs != 0:
+            return
+        sub = os.path.join(self.root_dir, f'cp_{epoch + 1}')
+        os.makedirs(sub, exist_ok=True)
+        path = os.path.join(sub, self.filename)
+        if not self.overwrite and os.path.exists(path):
+            return
+        self.model._sync_trained_weights()
+        self.model.network.save_weights(path)
+
+
 def check(rc, what):
     if rc == 0:
         return
