@@ -64,6 +64,10 @@ def main():
     ap.add_argument('--mh-draws', type=int, default=20000)
     ap.add_argument('--mh-tune', type=int, default=40000)
     ap.add_argument('--f32-eval', action='store_true', help='also sample the posterior with the exact-f32 network')
+    ap.add_argument('--test-source', default='train-generator', choices=['train-generator', 'independent'],
+                    help='train-generator: unseen TACs from the training generator (same per-ROI noise level as the '
+                         'training set, the likelihood the network learned); independent: a TAC with its own noise '
+                         'draw, like the reference\'s separately simulated test set')
     args = ap.parse_args()
 
     from pet_posterior_distribution_amd import Adam, ExponentialDecay, ImprovedDDPM, UnetConditional, glorot_uniform_init
@@ -119,11 +123,22 @@ def main():
     model.close()
 
     evals = []
-    for k in range(args.eval_tacs):
-        seed = 100 + k
-        cond, truth = make_condition(seed, prior, return_truth=True)
-        P = mh_problem(seed, prior)
-        rec = {'tac_seed': seed}
+    if args.test_source == 'train-generator':
+        # the training set's per-ROI noise draw (dataset_sigma_noise under the same seed), unseen sample indices
+        t = simulate_dataset(args.eval_tacs, prior, seed=11, sample_offset=1 << 40)
+        tests = []
+        for k in range(args.eval_tacs):
+            cond = t['condition'][k].cpu().numpy()
+            P = dict(time_vector=t['time_vector'], tac_ref=t['vartacref'][k].cpu().numpy(), k2p=float(prior['mu_k2p']),
+                     y_obs=cond[:48].astype(np.float64), sigma_noise=t['sigma_noise'], mu_DVR=prior['mu_DVR'],
+                     Cov_DVR=prior['Cov_DVR'], mu_R1=prior['mu_R1'], Cov_R1=prior['Cov_R1'])
+            tests.append((k, cond, P, {'DVR': t['varDVR'][k].cpu().numpy(), 'R1': t['varR1'][k].cpu().numpy()}))
+    else:
+        tests = [(100 + k,) + (lambda ct: (ct[0], mh_problem(100 + k, prior), ct[1]))(
+            make_condition(100 + k, prior, return_truth=True)) for k in range(args.eval_tacs)]
+    summary['test_source'] = args.test_source
+    for k, (seed, cond, P, truth) in enumerate(tests):
+        rec = {'tac': seed}
         samplers = [('bf16', 'bfloat16')] + ([('f32', 'float32')] if args.f32_eval and k == 0 else [])
         mh = MetropolisSRTM2(**P)
         mh.run(4, 2, 0, seed=1)
@@ -152,6 +167,16 @@ def main():
                  'norm_diff': {name: {q: {'mean': round(float(np.mean(met[name][q]['Norm_diff'])), 5),
                                           'max': round(float(np.max(met[name][q]['Norm_diff'])), 5)}
                                       for q in ('mu', 'std')} for name in ('DVR', 'R1')},
+                 'std_ratio_nn_over_mcmc_mean': {
+                     name: round(float(np.mean(met[name]['std']['NN'] / met[name]['std']['MCMC'])), 4)
+                     for name in ('DVR', 'R1')},
+                 # calibration against the simulation truth: |truth - mean| / SD (0.80 for a calibrated
+                 # Gaussian posterior) and the share of ROIs whose truth lies within one SD (0.68)
+                 'calibration': {
+                     meth: {name: {'mean_abs_z': round(float(np.mean(z)), 4), 'within_1sd': round(float(np.mean(z < 1)), 4)}
+                            for name, z in ((nm, np.abs(truth[nm][:, None] - met[nm]['mu'][meth]) / met[nm]['std'][meth])
+                                            for nm in ('DVR', 'R1'))}
+                     for meth in ('NN', 'MCMC')},
                  'ess_mean': {kk: [round(float(v[:, p].mean()), 1) for p in range(2)] for kk, v in ess.items()},
                  'posterior_mean_abs_err_vs_truth': {
                      'DVR': round(float(np.mean(np.abs(xs[..., 0].mean(0) - truth['DVR']))), 5),
