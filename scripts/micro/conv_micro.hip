@@ -34,8 +34,15 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
   bf16 *s1, *s2 = nullptr, *w, *out, *pool;
   float *cmap, *tmap, *bias;
   CK(hipMalloc(&s1, rows_in * c1 * 2));
-  if (c2) CK(hipMalloc(&s2, rows_in * c2 * 2));
-  const size_t wbytes = (size_t)(cout / G::NT) * NC * G::B_BYTES;
+  const size_t rows_in2 = G::FUSED ? (size_t)B * G::LH : rows_in;   // fused: src2 = the coarse input b
+  if (c2) CK(hipMalloc(&s2, rows_in2 * c2 * 2));
+  const int n1 = c1 / G::KC, n2 = c2 / G::KC;
+  const size_t wbytes = G::FUSED ? (size_t)(cout / G::NT) * (n1 * G::B_BYTES + n2 * G::B2_BYTES)
+                                 : (size_t)(cout / G::NT) * NC * G::B_BYTES;
+  bf16* ep = nullptr;
+  const size_t ebytes = (size_t)(cout / G::NT) * (n2 > 0 ? n2 : 1) * 2 * G::NT * G::ROWB;
+  CK(hipMalloc(&ep, ebytes));
+  fill_bf16<<<1024, 256>>>(ep, ebytes / 2, 11);
   CK(hipMalloc(&w, wbytes));
   CK(hipMalloc(&out, rows_out * cout * 2));
   CK(hipMalloc(&pool, rows_out * cout));
@@ -43,7 +50,7 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
   CK(hipMalloc(&tmap, (size_t)1000 * G::L * cout * 4));
   CK(hipMalloc(&bias, cout * 4));
   fill_bf16<<<1024, 256>>>(s1, rows_in * c1, 1);
-  if (c2) fill_bf16<<<1024, 256>>>(s2, rows_in * c2, 2);
+  if (c2) fill_bf16<<<1024, 256>>>(s2, rows_in2 * c2, 2);
   fill_bf16<<<1024, 256>>>(w, wbytes / 2, 3);
   fill_f32<<<1024, 256>>>(cmap, (size_t)G::L * cout, 4);
   fill_f32<<<1024, 256>>>(tmap, (size_t)1000 * G::L * cout, 5);
@@ -69,9 +76,26 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
   a.fin.wf = wf; a.fin.bf = bfv; a.fin.n_out = 4; a.fin.x_t = xt; a.fin.z = nullptr; a.fin.rng = rng;
   a.fin.rng_step = 3; a.fin.tab = tab; a.fin.T = 1000; a.fin.learn_mode = 2; a.fin.param_mode = 0;
   a.fin.flag_var_tilde = 1; a.fin.x_next = xn;
+  a.epack = ep;
+  // fused next-step down0 (final level): weights, maps and the s0 / p0 outputs
+  float *w0, *m0c, *m0t;
+  bf16 *s0n, *p0n;
+  CK(hipMalloc(&w0, 6 * 2 * 128 * 4));
+  CK(hipMalloc(&m0c, 48 * 128 * 4));
+  CK(hipMalloc(&m0t, (size_t)1000 * 48 * 128 * 4));
+  CK(hipMalloc(&s0n, (size_t)B * 48 * 128 * 2));
+  CK(hipMalloc(&p0n, (size_t)B * 24 * 128 * 2));
+  fill_f32<<<64, 256>>>(w0, 6 * 2 * 128, 12);
+  fill_f32<<<64, 256>>>(m0c, 48 * 128, 13);
+  fill_f32<<<1024, 256>>>(m0t, (size_t)1000 * 48 * 128, 14);
+  a.fin.next.x = xn; a.fin.next.w0 = w0; a.fin.next.cmap = m0c; a.fin.next.tmap = m0t;
+  a.fin.next.tac = nullptr; a.fin.next.tvec = nullptr; a.fin.next.t_uniform = G::EPI == EPI_FINAL ? 499 : -1;
+  a.fin.next.s0 = s0n; a.fin.next.p0 = p0n; a.fin.next.B = B;
   unsigned long long* dbg;
-  CK(hipMalloc(&dbg, 6 * 4096 * 8));
-  CK(hipMemset(dbg, 0, 6 * 4096 * 8));
+  // stamps [0, 8192 + 4 * grid) plus, on the final level, the keep_all_xt rows it writes through x_all
+  const size_t dbg_bytes = 6 * 4096 * 8 + (size_t)B * 96 * 4;
+  CK(hipMalloc(&dbg, dbg_bytes));
+  CK(hipMemset(dbg, 0, dbg_bytes));
 #if CONV_EXP_MODE & 128
   a.fin.x_all = reinterpret_cast<float*>(dbg);
 #endif
@@ -96,7 +120,8 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
     for (int b = 0; b < nb; ++b) { cyc.push_back((double)h[2 * b]); clk.push_back(h[2 * b] / (h[2 * b + 1] * 1e-8) * 1e-9); }
     std::sort(cyc.begin(), cyc.end());
     std::sort(clk.begin(), clk.end());
-    const double nmfma = (double)(c1 + c2) / G::KC * G::TAPS * (G::ROWB / 32) * 6;
+    const double nmfma = G::FUSED ? ((double)c1 / G::KC * G::TAPS + (double)c2 / G::KC * G::TAPS2) * (G::ROWB / 32) * 6
+                                  : (double)(c1 + c2) / G::KC * G::TAPS * (G::ROWB / 32) * 6;
     std::vector<unsigned long long> t4(4 * nb);
     CK(hipMemcpy(t4.data(), dbg + 8192, 4 * nb * 8, hipMemcpyDeviceToHost));
     unsigned long long tmin = ~0ull, tmax = 0;
@@ -127,16 +152,28 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
            cyc[nb / 2] / nmfma, clk[nb / 2], clk[0], clk[nb - 1]);
   }
 #endif
-  const double flop = 2.0 * rows_out * cout * (double)(c1 + c2) * G::TAPS;
+  const double flop = G::FUSED ? 2.0 * rows_out * cout * ((double)c1 * G::TAPS + (double)c2 * G::TAPS2)
+                               : 2.0 * rows_out * cout * (double)(c1 + c2) * G::TAPS;
   printf("%-12s mode %d  %8.2f us  %7.1f TF/s (executed)  grid %d\n", name, CONV_EXP_MODE, us, flop / us * 1e-6,
          ((B + G::S - 1) / G::S) * (cout / G::NT));
   hipFree(s1); if (s2) hipFree(s2); hipFree(w); hipFree(out); hipFree(pool); hipFree(cmap); hipFree(tmap);
   hipFree(bias); hipFree(wf); hipFree(bfv); hipFree(xt); hipFree(xn); hipFree(tab); hipFree(rng); hipFree(dbg);
+  hipFree(ep); hipFree(w0); hipFree(m0c); hipFree(m0t); hipFree(s0n); hipFree(p0n);
 }
 
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 1024;
   const int it = 200;
+  const char* only = argc > 2 ? argv[2] : "";
+  if (only[0] == 'f') {   // the product's 16-bit step: down layers + fused up levels
+    run<LK_DOWN1>("down1", B, 128, 0, 256, it);
+    run<LK_DOWN2>("down2", B, 256, 0, 512, it);
+    run<LK_DOWN3>("down3", B, 512, 0, 1024, it);
+    run<LK_UP0_F>("up0.fused", B, 512, 1024, 512, it);
+    run<LK_UP1_F>("up1.fused", B, 256, 512, 256, it);
+    run<LK_UP2_F>("up2.fused", B, 128, 256, 128, it);
+    return 0;
+  }
   run<LK_DOWN1>("down1", B, 128, 0, 256, it);
   run<LK_DOWN2>("down2", B, 256, 0, 512, it);
   run<LK_DOWN3>("down3", B, 512, 0, 1024, it);

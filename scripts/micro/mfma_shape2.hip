@@ -3,7 +3,8 @@
 // full mantissas (normal-like values), so the DVFS give-back of MI355X_MICROARCH.md item 7 shows.
 //   32x32x16: per 32-deep k: 2 x (3 A + 2 B reads, 6 MFMAs)
 //   16x16x32: per 32-deep k: 6 A + 4 B reads, 24 MFMAs
-// Same FLOP and the same LDS bytes per k for both.  Prints wall TF/s and the in-kernel clock
+// Same FLOP and the same LDS bytes per k for both.  Conflict-free swizzles: 32-row fragments piece ^ (row>>2)&3,
+// 16-row fragments piece ^ ((row>>2)&1)*2 (any row shift).  Prints wall TF/s and the in-kernel clock
 // (s_memtime / s_memrealtime, stamps into their own buffer).
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -26,7 +27,10 @@ __global__ __launch_bounds__(256, 1) void kshape(const uint4* src, float* out, u
   const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   float s = 0.f;
   if constexpr (SHAPE == 32) {
-    f32x16 acc[3][2] = {};
+    f32x16 acc[3][2];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 2; ++j)
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = out[i + j + e];
     const int lr = lane & 31, hk = lane >> 5;   // row, k half (8 elements)
     bf16x8 a[2][3], b[2][2];                    // fragments of step s (software-pipelined by one step)
     auto rd = [&](int step, bf16x8 (&aa)[3], bf16x8 (&bb)[2]) {
@@ -63,7 +67,9 @@ __global__ __launch_bounds__(256, 1) void kshape(const uint4* src, float* out, u
     }
     for (int i = 0; i < 3; ++i) for (int j = 0; j < 2; ++j) for (int e = 0; e < 16; ++e) s += acc[i][j][e];
   } else {
-    f32x4 acc[6][4] = {};
+    f32x4 acc[6][4];
+    for (int i = 0; i < 6; ++i)       // opaque initial values: no zero-peeled first iteration
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{out[i], out[j], out[i + j], out[0]};
     const int lr = lane & 15, q = lane >> 4;    // row, k quarter (8 elements of 32)
     bf16x8 a[2][6], b[2][4];
     auto rd = [&](int it, bf16x8 (&aa)[6], bf16x8 (&bb)[4]) {
@@ -71,12 +77,12 @@ __global__ __launch_bounds__(256, 1) void kshape(const uint4* src, float* out, u
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
         const int row = (rb + i * 16 + lr) & (LDS_ROWS - 1);
-        aa[i] = *reinterpret_cast<const bf16x8*>(&lds[row * 4 + (q ^ ((row >> 2) & 3))]);
+        aa[i] = *reinterpret_cast<const bf16x8*>(&lds[row * 4 + (q ^ (((row >> 2) & 1) << 1))]);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int row = (rb + 256 + j * 16 + lr) & (LDS_ROWS - 1);
-        bb[j] = *reinterpret_cast<const bf16x8*>(&lds[row * 4 + (q ^ ((row >> 2) & 3))]);
+        bb[j] = *reinterpret_cast<const bf16x8*>(&lds[row * 4 + (q ^ (((row >> 2) & 1) << 1))]);
       }
     };
     rd(0, a[0], b[0]);
