@@ -151,16 +151,35 @@ __device__ __forceinline__ void philox_normal2(unsigned long long seed, unsigned
 // p_sample epilogue (diffusion_model.py:424-496, 651-663), fp32, no FMA
 // contraction so every op rounds like the TF graph.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void p_sample_elem(const FinalArgs& f, int t, float x, float mo,
+// The per-timestep table values p_sample needs, loaded once per row ahead of the row loop
+// (their latency then hides behind the C-tile staging instead of stalling each row).
+struct PCoef {
+  float min_log, max_log;   // learn_ranged: [plvc, log beta]; fixed: [logvar_tilde, logvar]
+  float ca, cb;             // x0 = ca * x - cb * model_out (eps / v parameterisations)
+  float c1, c2;             // q_posterior_mean_variance coefficients
+};
+__device__ __forceinline__ PCoef load_pcoef(const FinalArgs& f, int t) {
+  const float* tab = f.tab;
+  const int T = f.T;
+  PCoef c;
+  c.min_log = tab[TAB_PLVC * T + t];
+  c.max_log = tab[TAB_LOG_BETA * T + t];
+  const bool v = f.param_mode == 2;
+  c.ca = tab[(v ? TAB_SQRT_AB : TAB_INV_SQRT_AB) * T + t];
+  c.cb = tab[(v ? TAB_SQRT_1M_AB : TAB_SQRT_RECIP_M1) * T + t];
+  c.c1 = tab[TAB_C1 * T + t];
+  c.c2 = tab[TAB_C2 * T + t];
+  return c;
+}
+
+__device__ __forceinline__ void p_sample_elem(const FinalArgs& f, const PCoef& pc, int t, float x, float mo,
                                                         float vv, float z, float* mean_o, float* var_o,
                                                         float* var_t_o) {
 #pragma clang fp contract(off)
-  const float* tab = f.tab;
-  const int T = f.T;
   float logvar, logvar_t;
   if (f.learn_mode == 2) {          // learn_ranged (:447-452)
-    const float min_log = tab[TAB_PLVC * T + t];
-    const float max_log = tab[TAB_LOG_BETA * T + t];
+    const float min_log = pc.min_log;
+    const float max_log = pc.max_log;
     const float frac = (vv + 1.0f) / 2.0f;
     logvar = frac * max_log + (1.0f - frac) * min_log;
     logvar_t = logvar;
@@ -168,27 +187,23 @@ __device__ __forceinline__ void p_sample_elem(const FinalArgs& f, int t, float x
     logvar = vv;
     logvar_t = vv;
   } else {                          // fixed (:455-462)
-    logvar = tab[TAB_LOG_BETA * T + t];
-    logvar_t = tab[TAB_PLVC * T + t];
+    logvar = pc.max_log;
+    logvar_t = pc.min_log;
   }
   float mean;
   if (f.param_mode == 3) {          // x_prev (:476-479)
     mean = mo;
   } else {
     float x0;
-    if (f.param_mode == 0) {        // eps (:370-374)
-      const float a = tab[TAB_INV_SQRT_AB * T + t] * x;
-      const float b = tab[TAB_SQRT_RECIP_M1 * T + t] * mo;
-      x0 = a - b;
-    } else if (f.param_mode == 2) { // v (:380-386)
-      const float a = tab[TAB_SQRT_AB * T + t] * x;
-      const float b = tab[TAB_SQRT_1M_AB * T + t] * mo;
+    if (f.param_mode == 0 || f.param_mode == 2) {   // eps (:370-374) / v (:380-386)
+      const float a = pc.ca * x;
+      const float b = pc.cb * mo;
       x0 = a - b;
     } else {                        // x0
       x0 = mo;
     }
-    const float m1 = tab[TAB_C1 * T + t] * x0;   // q_posterior_mean_variance (:415)
-    const float m2 = tab[TAB_C2 * T + t] * x;
+    const float m1 = pc.c1 * x0;    // q_posterior_mean_variance (:415)
+    const float m2 = pc.c2 * x;
     mean = m1 + m2;
   }
   const float mask = (t == 0) ? 0.0f : 1.0f;
@@ -310,7 +325,10 @@ struct ConvGeom {
   static constexpr int MAP_PIECES = L * NT / 4;                       // 16-B pieces of one map
   static constexpr int C_PIECE0 = (MAP_PIECES + 63) / 64 * 64;        // label map starts wave-instr aligned
   static constexpr int MAP_OFF = RING;
-  static constexpr int MAP_BYTES = PREMAP ? (C_PIECE0 + MAP_PIECES) * 16 : 0;
+  // map pieces per wave when every wave issues the same count (fused levels: the first ring barrier
+  // then waits for chunk 0 only, vmcnt(NPI_MAP)); the region is padded to whole block instructions
+  static constexpr int NPI_MAP = (C_PIECE0 + MAP_PIECES + kThreads - 1) / kThreads;
+  static constexpr int MAP_BYTES = PREMAP ? (FUSED ? NPI_MAP * kThreads : C_PIECE0 + MAP_PIECES) * 16 : 0;
   static constexpr int TAC_OFF = MAP_OFF + MAP_BYTES;
   static constexpr int TAIL = PREMAP ? TAC_OFF + (S + 1) * 4 : 0;
   static_assert(S <= 64, "one wave gathers the block's condition indices");
@@ -319,8 +337,12 @@ struct ConvGeom {
   // lanes read consecutive rows conflict-free) prefetched behind the ring at kernel start
   static constexpr bool FIN_MAPS = FUSED && EPI == EPI_FINAL;
   static constexpr int FMAP_PIECES = L * (FIN_LD / 4);                 // per map, incl. one pad piece per row
+  // both maps as one array of 2 FMAP_PIECES pieces: every wave issues FMAP_FULL block instructions,
+  // waves with wv * 64 < FMAP_REM one more (its lanes past the end land in the padding)
+  static constexpr int FMAP_STRIDE = FMAP_PIECES;                      // pieces between the two maps
+  static constexpr int FMAP_FULL = 2 * FMAP_PIECES / kThreads, FMAP_REM = 2 * FMAP_PIECES - FMAP_FULL * kThreads;
   static constexpr int FMAP_OFF = (SMEM0 + 15) / 16 * 16;
-  static constexpr int FMAP_BYTES = FIN_MAPS ? 2 * FMAP_PIECES * 16 : 0;
+  static constexpr int FMAP_BYTES = FIN_MAPS ? (FMAP_FULL * kThreads + (FMAP_REM + 63) / 64 * 64) * 16 : 0;
   static constexpr int SMEM1 = SMEM0 > TAIL ? SMEM0 : TAIL;
   static constexpr int SMEM = FIN_MAPS ? FMAP_OFF + FMAP_BYTES : SMEM1;
   static_assert(!FIN_MAPS || (TAIL == 0 && FIN_LD == 132 && NT == 128), "final map layout");
@@ -687,6 +709,41 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
   const int m0 = m_tile * G::S;
 
   const int NC = a.c1 / G::KC + a.c2 / G::KC;
+
+  // Final level: this thread's output row (one per thread) and every global operand of its
+  // p_sample, loaded at kernel start.  They are older than every LDS-DMA of the K loop, so the
+  // ring's counted waits retire them for free, and the row loop after the K loop waits on LDS only
+  // (a dependent global load there cost a full memory round trip per row).
+  const FinalArgs& fa = a.fin;
+  const int s_me = tid / L, l_me = tid - s_me * L, b_me = m0 + s_me;
+  const bool row_ok = EPI == EPI_FINAL && tid < G::MT && b_me < B;
+  const int bq = row_ok ? b_me : m0;
+  const bool do_ps = fa.net_out == nullptr;
+  int t_me = 0, tac_me = 0;
+  size_t idx_me = 0;
+  float bfin[4] = {0.f, 0.f, 0.f, 0.f}, xt_me[2] = {0.f, 0.f}, z_me[2] = {0.f, 0.f};
+  PCoef pc{};
+  unsigned long long rng0 = 0, rng1 = 0;
+  if constexpr (EPI == EPI_FINAL) {
+    static_assert(EPI != EPI_FINAL || G::MT <= kThreads, "one final row per thread");
+    t_me = a.t_uniform >= 0 ? a.t_uniform : a.tvec[bq];
+    tac_me = a.tac ? a.tac[bq] : 0;
+    idx_me = ((size_t)bq * L + (row_ok ? l_me : 0)) * 2;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bfin[q] = q < fa.n_out ? fa.bf[q] : 0.f;
+    if (do_ps) {
+      xt_me[0] = fa.x_t[idx_me];
+      xt_me[1] = fa.x_t[idx_me + 1];
+      if (fa.z) {
+        z_me[0] = fa.z[idx_me];
+        z_me[1] = fa.z[idx_me + 1];
+      } else {
+        rng0 = fa.rng[0];
+        rng1 = fa.rng[1];
+      }
+      pc = load_pcoef(fa, t_me);
+    }
+  }
 
   // zero row of every stage
   if (tid < G::STAGES * G::CPR) {
@@ -1139,32 +1196,49 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
   const bool pre_t = G::PREMAP && a.tmap && a.t_uniform >= 0;
   const bool pre_c = G::PREMAP && a.cmap;
   int tac0 = 0;
+  int tb_pre = 0;   // fused levels: wave 0's per-sample condition indices, read before any DMA
+  if constexpr (G::PREMAP && G::FUSED) {
+    if (a.tac) tac0 = a.tac[min(m0, B - 1)];
+    tb_pre = (a.tac && tid < 64 && m0 + tid < B) ? a.tac[m0 + tid] : tac0;
+  }
   auto prefetch_maps = [&]() {
     if constexpr (G::PREMAP) {
-      if (a.tac) tac0 = a.tac[min(m0, B - 1)];
+      if (!G::FUSED && a.tac) tac0 = a.tac[min(m0, B - 1)];
       if (tid < 64) {            // wave 0: condition indices of the block's samples (S <= 64)
         const int b = m0 + tid;
-        const int tb = (a.tac && b < B) ? a.tac[b] : tac0;
+        const int tb = G::FUSED ? tb_pre : (a.tac && b < B) ? a.tac[b] : tac0;
         if (tid < G::S) reinterpret_cast<int*>(smem + G::TAC_OFF)[tid] = tb;
         const unsigned long long other = __ballot(tid < G::S && tb != tac0);
         if (tid == 0) reinterpret_cast<int*>(smem + G::TAC_OFF)[G::S] = other != 0ull;
       }
       const i32x4 rs_t = make_rsrc(a.tmap, (unsigned)a.n_t * L * (unsigned)a.cout * 4u);
       const i32x4 rs_c = make_rsrc(a.cmap, (unsigned)a.n_tac * L * (unsigned)a.cout * 4u);
-      constexpr int NPI = (G::C_PIECE0 + G::MAP_PIECES + kThreads - 1) / kThreads;
+      constexpr int NPI = G::NPI_MAP;
 #pragma unroll
       for (int k = 0; k < NPI; ++k) {
         const int p0 = k * kThreads + wv * 64;
         const bool is_c = p0 >= G::C_PIECE0;
-        if (is_c ? !pre_c : !pre_t) continue;
+        const bool on = is_c ? pre_c : pre_t;
         const int q = p0 + lane - (is_c ? G::C_PIECE0 : 0);
-        if (q < G::MAP_PIECES) {
+        if constexpr (G::FUSED) {
+          // exactly NPI instructions per wave: the first ring barrier counts them (vmcnt(NPI))
           const int l = q / (NT / 4), c = q - l * (NT / 4);
           const int row = is_c ? tac0 : a.t_uniform;
-          const int off = (((row * L + l) * a.cout) + n_tile * NT + c * 4) * 4;
+          const int off = (on && q < G::MAP_PIECES) ? (((row * L + l) * a.cout) + n_tile * NT + c * 4) * 4
+                                                    : 0x7ffffff0;   // out of range: the DMA lands zeros
           llvm_amdgcn_raw_buffer_load_lds(is_c ? rs_c : rs_t,
                                           (__attribute__((address_space(3))) void*)(smem + G::MAP_OFF + p0 * 16), 16,
                                           off, 0, 0, 0);
+        } else {
+          if (!on) continue;
+          if (q < G::MAP_PIECES) {
+            const int l = q / (NT / 4), c = q - l * (NT / 4);
+            const int row = is_c ? tac0 : a.t_uniform;
+            const int off = (((row * L + l) * a.cout) + n_tile * NT + c * 4) * 4;
+            llvm_amdgcn_raw_buffer_load_lds(is_c ? rs_c : rs_t,
+                                            (__attribute__((address_space(3))) void*)(smem + G::MAP_OFF + p0 * 16), 16,
+                                            off, 0, 0, 0);
+          }
         }
       }
     }
@@ -1177,32 +1251,38 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
   using Seg2 = std::integral_constant<int, 2>;
   // fused final level, t uniform and one condition in the tile: map rows into LDS (FMAP_OFF)
   bool fin_fast = false;
+  int tac0f = 0;
+  if constexpr (G::FIN_MAPS) {   // read before any DMA is issued: waiting on them retires nothing else
+    tac0f = a.tac ? a.tac[min(m0, B - 1)] : 0;
+    fin_fast = a.t_uniform >= 0 && a.tmap && a.cmap;
+    if (a.tac)
+      for (int k = 1; k < G::S; ++k) fin_fast = fin_fast && (m0 + k >= B || a.tac[m0 + k] == tac0f);
+  }
   auto prefetch_fin_maps = [&]() {
     if constexpr (G::FIN_MAPS) {
-      const int tac0f = a.tac ? a.tac[min(m0, B - 1)] : 0;
-      fin_fast = a.t_uniform >= 0 && a.tmap && a.cmap;
-      if (a.tac)
-        for (int k = 1; k < G::S; ++k) fin_fast = fin_fast && (m0 + k >= B || a.tac[m0 + k] == tac0f);
-      if (!fin_fast) return;
       const i32x4 rs_t = make_rsrc(a.tmap, (unsigned)a.n_t * L * (unsigned)a.cout * 4u);
       const i32x4 rs_c = make_rsrc(a.cmap, (unsigned)a.n_tac * L * (unsigned)a.cout * 4u);
-      constexpr int NPI = (G::FMAP_PIECES + kThreads - 1) / kThreads;
+      // a fixed number of instructions per wave (the first ring barrier counts them); pieces past
+      // the maps, or every piece when the maps are not used (fin_fast false), read out of range
+      auto piece = [&](int k) {
+        const int p0 = k * kThreads + wv * 64, qq = p0 + lane;
+        const int mp = qq >= G::FMAP_PIECES, q = qq - mp * G::FMAP_PIECES;
+        const int l = q / (G::FIN_LD / 4), c = min(q - l * (G::FIN_LD / 4), NT / 4 - 1);   // pad piece: a copy
+        const int row = mp ? tac0f : a.t_uniform;
+        const int off = (fin_fast && qq < 2 * G::FMAP_PIECES) ? ((row * L + l) * a.cout + c * 4) * 4 : 0x7ffffff0;
+        llvm_amdgcn_raw_buffer_load_lds(mp ? rs_c : rs_t,
+                                        (__attribute__((address_space(3))) void*)(smem + G::FMAP_OFF + p0 * 16), 16,
+                                        off, 0, 0, 0);
+      };
 #pragma unroll
-      for (int mp = 0; mp < 2; ++mp)
-#pragma unroll
-        for (int k = 0; k < NPI; ++k) {
-          const int p0 = k * kThreads + wv * 64, q = p0 + lane;
-          if (q < G::FMAP_PIECES) {
-            const int l = q / (G::FIN_LD / 4), c = min(q - l * (G::FIN_LD / 4), NT / 4 - 1);   // pad piece: a copy
-            const int row = mp ? tac0f : a.t_uniform;
-            llvm_amdgcn_raw_buffer_load_lds(mp ? rs_c : rs_t,
-                                            (__attribute__((address_space(3))) void*)(smem + G::FMAP_OFF +
-                                                                                        (mp * G::FMAP_PIECES + p0) * 16),
-                                            16, ((row * L + l) * a.cout + c * 4) * 4, 0, 0, 0);
-          }
-        }
+      for (int k = 0; k < G::FMAP_FULL; ++k) piece(k);
+      if (wv * 64 < G::FMAP_REM) piece(G::FMAP_FULL);
     }
   };
+  // LDS-DMA instructions per wave issued by the two prefetches (fused levels): NMAPW, or NMAPW + 1
+  // for the waves that issue the final maps' partial instruction
+  constexpr int NMAPW = (G::PREMAP && G::FUSED ? G::NPI_MAP : 0) + (G::FIN_MAPS ? G::FMAP_FULL : 0);
+  const bool map_extra = G::FIN_MAPS && wv * 64 < G::FMAP_REM;
   using Seg2Next = std::integral_constant<int, 3>;
   if constexpr (G::FUSED) {
     // Fused up level: segment-1 chunks (skip s), then segment-2 chunks (coarse b); every
@@ -1235,7 +1315,15 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
       dma.all(smem, 0, 0, lane);
       prefetch_maps();
       prefetch_fin_maps();
-      ring_barrier<0>();
+      // B0: chunk 0 landed; the maps (issued after it, NMAPW per wave) may still be in flight --
+      // B1 below retires them together with chunk 1, long before the epilogue reads them
+      static_assert(NMAPW + 1 + 2 * G::PER < 64 && NMAPW + 1 + 2 * G::PER2 < 64, "vmcnt range");
+      if (map_extra) ring_barrier<NMAPW + 1>();
+      else ring_barrier<NMAPW>();
+#if CONV_EXP_MODE & 128
+      st_c0 = __builtin_amdgcn_s_memtime();
+      st_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
       compute(smem, Two{}, 1, 1, Seg1{}, 0, P0{});              // chunks 1, 2 -> stages 1, 2
       ring_barrier<G::PER>();
       int buf = 1, kc = 1;
@@ -1608,12 +1696,15 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
       for (int k = 0; k < 6; ++k) mv[k] = tm[tid + kThreads * k] + cm[tid + kThreads * k];
     }
     __syncthreads();
-    for (int r = tid; r < G::MT; r += kThreads) {
-      const int s = r / L, l = r - s * L, b = m0 + s;
-      if (b >= B) continue;
-      if constexpr ((FIN_EXP & 4) != 0) { xst[r * 2] = xst[r * 2 + 1] = fin[r * G::FIN_LD]; continue; }
-      const int tac = a.tac ? a.tac[b] : 0;
-      const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[b];
+#if CONV_EXP_MODE & 128
+    if (tid == 0) reinterpret_cast<unsigned long long*>(a.fin.x_all)[4096 + 2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
+    // one Philox call yields the Box-Muller pair for both parameters of this ROI (its key landed
+    // during the staging above; pure ALU from here)
+    if (do_ps && !f.z && row_ok) philox_normal2(rng0, rng1 + (unsigned long long)b_me, f.rng_step, l_me, z_me);
+    if (row_ok) {
+      const int r = tid, l = l_me, b = b_me, t = t_me, tac = tac_me;
+      if constexpr ((FIN_EXP & 4) != 0) { xst[r * 2] = xst[r * 2 + 1] = fin[r * G::FIN_LD]; goto fin_rows_done; }
       const float* mp = a.tmap ? a.tmap + ((size_t)t * L + l) * cout : nullptr;
       const float* cp = a.cmap ? a.cmap + ((size_t)tac * L + l) * cout : nullptr;
       f32x4 o4 = {0.f, 0.f, 0.f, 0.f};
@@ -1636,48 +1727,44 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
       };
       if (G::FIN_MAPS && fin_fast) {                 // the same map rows, prefetched into LDS
         const float* lm = reinterpret_cast<const float*>(smem + G::FMAP_OFF) + l * G::FIN_LD;
-        dot(lm, lm + G::FMAP_PIECES * 4);
+        dot(lm, lm + G::FMAP_STRIDE * 4);
       } else {
         dot(mp, cp);
       }
       float o[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) o[q] = o4[q] + (q < n_out ? f.bf[q] : 0.f);
-      if (f.net_out) {
+      for (int q = 0; q < 4; ++q) o[q] = o4[q] + bfin[q];
+      if (!do_ps) {
         for (int q = 0; q < n_out; ++q) f.net_out[((size_t)b * L + l) * n_out + q] = o[q];
-        continue;
+        goto fin_rows_done;
       }
-      // one Philox call yields the Box-Muller pair for both parameters of this ROI
-      float z[2];
-      const size_t idx = ((size_t)b * L + l) * 2;
-      if (f.z) {
-        z[0] = f.z[idx];
-        z[1] = f.z[idx + 1];
-      } else {
-        philox_normal2(f.rng[0], f.rng[1] + (unsigned long long)b, f.rng_step, l, z);
-      }
+      const size_t idx = idx_me;
       const int half = n_out / 2;
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const float mo = o[c];
         const float vv = n_out == 4 ? o[half + c] : 0.f;
         float mean, var, var_t;
-        p_sample_elem(f, t, f.x_t[idx + c], mo, vv, z[c], &mean, &var, &var_t);
+        p_sample_elem(f, pc, t, xt_me[c], mo, vv, z_me[c], &mean, &var, &var_t);
         if (f.mean_out) f.mean_out[idx + c] = mean;
         if (f.var_out) f.var_out[idx + c] = var;
         if (f.var_tilde_out) f.var_tilde_out[idx + c] = var_t;
         if (f.x_next) {
           const float xn = mean + (f.flag_var_tilde ? var_t : var);
           f.x_next[idx + c] = xn;
-          if (f.x_all) f.x_all[idx + c] = xn;
+          if (f.x_all && !(CONV_EXP_MODE & 128)) f.x_all[idx + c] = xn;   // (diagnostic builds: x_all holds stamps)
           xst[r * 2 + c] = xn;
         }
       }
     }
+  fin_rows_done:
     if (fuse_next) {
       // down0 of the next reverse step on this tile's samples (x_next from LDS): the
       // same per-position code as down0_kernel, 16 positions in flight per pass.
       __syncthreads();                               // x_next rows staged; C tile dead
+#if CONV_EXP_MODE & 128
+      if (tid == 0) reinterpret_cast<unsigned long long*>(a.fin.x_all)[4096 + 2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
       const bool fast = *flag != 0;
       float* mp = fin;
       if (fast) {
@@ -1686,6 +1773,11 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
       }
       __syncthreads();
       if constexpr (!(FIN_EXP & 1)) down0_positions<T>(nd, xst, mp, fast, m0, nb_next, wr, n0_next, tid >> 4, kThreads / 16);
+#if CONV_EXP_MODE & 128
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) reinterpret_cast<unsigned long long*>(a.fin.x_all)[8192 + 4 * blockIdx.x + 3] = __builtin_amdgcn_s_memrealtime();
+#endif
     }
   }
 }
