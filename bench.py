@@ -445,6 +445,39 @@ def mh_slice_and_protocol(iddpm_10k_s, dev):
              'iddpm_speedup_over_mh': round(proto / iddpm_10k_s, 2), 'reference_claim': '> 230x (README.md:12)'})
 
 
+def weights_sensitivity(net, cond, B, dev, reps=3):
+    """The step's speed depends on the weight VALUES: the chip holds its clock by power under this load, and
+    MFMA energy depends on operand bit activity.  Same workload as `value` with all-zero weights (the power
+    floor: MFMA operands toggle nothing) and, when scripts/train_protocol.py's output is present, with the
+    trained network (weights/trained_r02.npz).  Context for `value`, which uses random-init weights."""
+    import torch
+    from pet_posterior_distribution_amd import ImprovedDDPM
+    from pet_posterior_distribution_amd.configs import shipped_diff_args
+    keep = net.weights
+    variants = {'zeros': {k: np.zeros_like(v) for k, v in keep.items()}}
+    tw = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'weights', 'trained_r02.npz')
+    if os.path.exists(tw):
+        with np.load(tw) as z:
+            variants['trained_r02'] = {k: z[k] for k in keep}
+    out = {}
+    try:
+        for name, w in variants.items():
+            net.weights = w
+            m = ImprovedDDPM(network=net, dtype='bfloat16', device=dev.index, **shipped_diff_args())
+            x = m.philox_normal(B, seed=1)
+            m.ddpm_loop(x, cond[None], seed=2)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                m.ddpm_loop(x, cond[None], seed=2)
+            torch.cuda.synchronize()
+            out[name + '_samples_per_s'] = round(reps * B / (time.perf_counter() - t0), 1)
+            m.close()
+    finally:
+        net.weights = keep
+    return out
+
+
 def iddpm_10k_seconds(model, cond):
     """One TAC's posterior as the reference draws it: n_posterior = chunk_size = 10,000 samples in one
     ddpm_loop (main_script.py:315-319, 414-420), graph warm-up then one timed run."""
@@ -592,6 +625,7 @@ def main():
             line['f32_exact'] = f32_exact_rate(cond[0], B, n_rev, dev)
             t10k = iddpm_10k_seconds(model, cond[0])
             line['mh_config3_slice'], line['reference_protocol'] = mh_slice_and_protocol(t10k, dev)
+            line['weights_sensitivity'] = weights_sensitivity(net, cond[0], B, dev)
         sm = allst[..., 1]
         line['posterior_mean_DVR_roi0'] = [round(float(v), 5) for v in sm[:, 0, 0]]
         print(json.dumps(line), flush=True)

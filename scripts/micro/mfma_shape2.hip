@@ -16,6 +16,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+#ifndef MFMA_ORDER
+#define MFMA_ORDER 0
+#endif
 constexpr int LDS_ROWS = 512;   // 512 rows x 64 B (32 bf16 of k) = 32 KB A/B image
 
 template <int SHAPE>
@@ -52,10 +55,17 @@ __global__ __launch_bounds__(256, 1) void kshape(const uint4* src, float* out, u
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         rd(st + u + 1, a[u ^ 1], b[u ^ 1]);
+#if MFMA_ORDER == 1   // B-major: each B fragment held for 3 consecutive MFMAs
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int i = 0; i < 3; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[u][i], b[u][j], acc[i][j], 0, 0, 0);
+#else                 // A-major (the conv kernel's order): each A fragment held for 2
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[u][i], b[u][j], acc[i][j], 0, 0, 0);
+#endif
         // M R M R M R M R M R M: one read per MFMA gap
 #pragma unroll
         for (int g = 0; g < 5; ++g) {
