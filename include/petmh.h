@@ -81,6 +81,15 @@ int petmh_run_draws(petmh_handle h, const double* x0_dev, int n_chains, int n_dr
  * state instead (textbook component-wise MH). */
 int petmh_set_sampler(petmh_handle h, int tune_interval, double scaling, int vs_sweep_start);
 
+/* Chain kernel (no reference counterpart: how the GPU runs mcmc.py:156-157's sampler).
+ *   kernel 0 = automatic (batched for <= 256 chains, else one update at a time),
+ *          1 = one element update at a time (one wave per chain),
+ *          2 = batched proposals (the 144 likelihoods a sweep can need, evaluated up front,
+ *              then a scan over the shuffled order; latency-optimised).
+ *   waves_per_chain (batched kernel only): 0 = automatic, or 1, 2, 4, 12.
+ * Both kernels take the same accept/reject path up to the summation order over frames. */
+int petmh_set_kernel(petmh_handle h, int kernel, int waves_per_chain);
+
 /* Joint log density of mcmc.py:147-155 at n points x_dev [n][2*n_roi] -> out_dev [n]. */
 int petmh_logp(petmh_handle h, const double* x_dev, int n, double* out_dev, void* stream);
 

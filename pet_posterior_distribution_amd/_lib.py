@@ -69,6 +69,7 @@ SYMBOLS = [
     ('petmh_run', C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_p, C.c_void_p,
                             C.c_void_p, C.c_void_p]),
     ('petmh_set_sampler', C.c_int, [C.c_void_p, C.c_int, C.c_double, C.c_int]),
+    ('petmh_set_kernel', C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     ('petmh_run_draws', C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_p,
                                   C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     ('petmh_logp', C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),

@@ -147,6 +147,7 @@ struct petmh_ctx {
   int tune_interval = 100;   // pymc Metropolis defaults
   double scaling = 1.0;
   int vs_sweep_start = 1;    // pymc 5.12 elemwise_update compares against the sweep-start point
+  int kernel = 0, wpc = 0;   // petmh_set_kernel
 };
 
 extern "C" {
@@ -234,6 +235,8 @@ int petmh_run_draws(petmh_handle h, const double* x0, int n_chains, int n_draws,
   r.accept = accept;
   r.last = last;
   r.draws = draws;
+  r.kernel = h->kernel;
+  r.wpc = h->wpc;
   HIPC(launch_mh_chains(h->c, r, (hipStream_t)stream));
   return 0;
 }
@@ -243,6 +246,16 @@ int petmh_set_sampler(petmh_handle h, int tune_interval, double scaling, int vs_
   h->tune_interval = tune_interval;
   h->scaling = scaling;
   h->vs_sweep_start = vs_sweep_start != 0;
+  return 0;
+}
+
+int petmh_set_kernel(petmh_handle h, int kernel, int waves_per_chain) {
+  if (!h || kernel < 0 || kernel > 2) return fail("bad kernel (0 auto, 1 one update at a time, 2 batched)");
+  if (!(waves_per_chain == 0 || waves_per_chain == 1 || waves_per_chain == 2 || waves_per_chain == 4 ||
+        waves_per_chain == 12))
+    return fail("waves_per_chain must be 0 (auto), 1, 2, 4 or 12");
+  h->kernel = kernel;
+  h->wpc = waves_per_chain;
   return 0;
 }
 

@@ -33,6 +33,8 @@ struct MHRun {
   double* accept;              // [n_chains][96] or null
   double* last;                // [n_chains][96] or null
   double* draws;               // [n_chains][n_draws][96] or null (kept draws)
+  int kernel;                  // petmh_set_kernel: 0 auto, 1 one update at a time, 2 batched
+  int wpc;                     // batched: waves per chain (0 auto)
 };
 
 hipError_t launch_mh_chains(const MHConst& c, const MHRun& r, hipStream_t s);

@@ -9,6 +9,8 @@
 // the MvNormal prior change is 2 d g_i + d^2 P_ii (g kept current on accept).
 #include "mh_internal.h"
 
+#include <cstdlib>
+
 // Tuning knobs (the product uses the defaults; scripts/micro/build_mh.sh builds variants)
 #ifndef MH_EXP_MODE
 #define MH_EXP_MODE 0     // timing experiments only: bits drop exp / log / log_ndtr / sqrt / divisions
@@ -323,6 +325,368 @@ __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Batched-proposal sampler (the default chain kernel).
+//
+// Within one draw every proposal is known before the sweep starts: element (v, i) proposes
+// x_i + Z_k s_k, whatever happened earlier in the sweep.  Its ROI-i likelihood depends on the
+// sweep only through the OTHER element of ROI i (proposed-and-accepted earlier, or not).  So the
+// three likelihoods a sweep can ask of ROI i,
+//   c = 0: (DVR', R1)   c = 1: (DVR, R1')   c = 2: (DVR', R1')
+// are evaluated up front for all 48 ROIs (144 evaluations, no sequential dependence: batches of
+// kQ evaluations share one operator-row read per frame and keep kQ independent FMA chains in
+// flight), and the sweep itself (pymc order, vs the sweep start) becomes a scan over
+// wave-uniform scalars that picks the evaluation each element needs.  Same expressions per
+// evaluation as roi_loglik (the operator row FMAs in the same order), so the chain path is the
+// oracle's up to the summation order over frames.
+//
+// WPC waves cooperate on one chain (the 144 evaluations are dealt to them, the scan runs
+// redundantly in every wave, identical decisions): WPC = 1 for throughput (10k chains),
+// WPC = kBW for few chains (the reference's 4-chain protocol is latency bound).
+// ---------------------------------------------------------------------------
+// diagnostic builds only (scripts/micro/build_mh.sh): bit 1 drops the per-frame transcendentals,
+// 2 the exponentials of e, 4 the operator FMAs, 8 the sweep scan, 16 the sweep's RNG + sort
+#ifndef MH_BEXP
+#define MH_BEXP 0
+#endif
+#ifndef MH_P_UNROLL
+#define MH_P_UNROLL 1
+#endif
+constexpr int kQ = 8;                 // evaluations per batch
+#ifndef MH_BW
+#define MH_BW 12
+#endif
+constexpr int kBW = MH_BW;            // waves per workgroup
+constexpr int kNE = 3 * NR;           // evaluations per draw
+
+struct LdsB {
+  double M[NF * MLD];
+  double Y[NR * NF], SIG[NR * NF];
+  double CR[NF], TV[NF];
+  double MUD[NR], MUR[NR];
+  double W[kBW][kQ * 64];             // per wave: e rows [q][MLD] / frame terms [q][64] / sweep draws
+  double P[kBW][kQ * 4];              // per wave: the batch's (R1, k2, k2a, roi)
+  double LL[kBW][kNE];                // per chain group: the draw's evaluations
+};
+
+// kQ log-likelihoods.  Lane q < kQ brings evaluation q's (roi, DVR, R1) in (my_roi, my_dvr,
+// my_r1); the results come back wave-uniform in out[q].  W / P: this wave's scratch.
+// mcmc.py:151-155 per frame; the 54-frame sum is a stride-8 partial per lane plus a 3-step DPP
+// tree inside each 8-lane group (lane 8 q + 7 ends with evaluation q).  The transcendental part
+// runs one evaluation at a time (not unrolled: the fp64 exp / log / erfc constants would
+// otherwise be hoisted into registers kQ times over); the operator FMAs run kQ chains at once.
+__device__ __forceinline__ void eval_batch(const LdsB& s, double* W, double* P, int lane, int my_roi, double my_dvr,
+                                           double my_r1, double k2p, double (&out)[kQ]) {
+  if (lane < kQ) {
+    const double k2 = k2p * my_r1;       // kinetic_model.py:153-154
+    P[lane * 4 + 0] = my_r1;
+    P[lane * 4 + 1] = k2;
+    P[lane * 4 + 2] = k2 / my_dvr;
+    P[lane * 4 + 3] = (double)my_roi;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  const int f = lane < NF ? lane : 0;
+  if (lane < MLD) {
+    const double tv = s.TV[f];
+#pragma unroll 1
+    for (int q = 0; q < kQ; ++q)
+      W[q * MLD + lane] = lane < NF ? ((MH_BEXP & 2) ? 1.0 - P[q * 4 + 2] * tv : exp(-P[q * 4 + 2] * tv)) : 0.0;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  double c0[kQ], c1[kQ];
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) c0[q] = c1[q] = 0.0;
+  if (lane < NF && !(MH_BEXP & 4)) {
+    const double2* mrow = reinterpret_cast<const double2*>(s.M + lane * MLD);
+#pragma unroll MH_P_UNROLL
+    for (int p = 0; p < MLD / 2; ++p) {
+      const double2 m = mrow[p];
+#pragma unroll
+      for (int q = 0; q < kQ; ++q) {
+        const double2 x = reinterpret_cast<const double2*>(W + q * MLD)[p];
+        c0[q] = fma(m.x, x.x, c0[q]);
+        c1[q] = fma(m.y, x.y, c1[q]);
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) W[q * 64 + lane] = c0[q] + c1[q];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  const double crf = s.CR[f];
+#pragma unroll 1
+  for (int q = 0; q < kQ; ++q) {
+    double l = 0.0;
+    if (lane < NF) {
+      const double r1 = P[q * 4 + 0], k2 = P[q * 4 + 1], k2a = P[q * 4 + 2];
+      const int i = (int)P[q * 4 + 3];
+      const double conv = W[q * 64 + lane];
+      const double tac = r1 * crf + (k2 - r1 * k2a) * conv;                // :157-158
+      const double sn = tac < 0.0 ? 1e-6 : tac;                           // mcmc.py:152
+#if MH_BEXP & 1
+      const double sig = sn * s.SIG[i * NF + lane];
+      const double z = (s.Y[i * NF + lane] - sn) * sig;
+      l = -0.5 * z * z - 0.9189385332046727 - sig;
+#else
+      const double sig = sqrt(sn) * s.SIG[i * NF + lane];                 // :153
+      const double inv = 1.0 / sig;
+      const double z = (s.Y[i * NF + lane] - sn) * inv;
+      const double xs = sn * inv;
+      // log Phi(xs) (log_ndtr): xs = sqrt(sn) / SIG >= 0 or NaN, so only its x > -1 branch
+      // log(erfc(-x / sqrt 2) / 2) is reachable (NaN falls through to NaN either way)
+      const double lnd = xs < 10.0 ? log(0.5 * erfc(-xs * 0.7071067811865476)) : 0.0;
+      l = -0.5 * z * z - 0.9189385332046727 - log(sig) - lnd;
+#endif
+    }
+    W[q * 64 + lane] = l;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  const int qq = lane >> 3, pp = lane & 7;
+  double sum = 0.0;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) sum += W[qq * 64 + pp + 8 * m];
+  sum += dpp_f64<0x111>(sum);          // row_shr:1
+  sum += dpp_f64<0x112>(sum);          // row_shr:2
+  sum += dpp_f64<0x114>(sum);          // row_shr:4 -> lanes 7 / 15 of each row: their 8-lane group
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) out[q] = lane_bcast(sum, 8 * q + 7);
+}
+
+template <int WPC>
+__global__ __launch_bounds__(kBW * 64) void mh_chain_batched(MHConst c, MHRun r) {
+  constexpr int CPG = kBW / WPC;       // chains per workgroup
+  __shared__ LdsB s;
+  for (int k = threadIdx.x; k < NF * MLD; k += blockDim.x) {
+    const int f = k / MLD, g = k - f * MLD;
+    s.M[k] = g < NF ? c.M[g * NF + f] : 0.0;   // global operator is [g][f]
+  }
+  for (int k = threadIdx.x; k < NR * NF; k += blockDim.x) { s.Y[k] = c.Y[k]; s.SIG[k] = c.SIG[k]; }
+  for (int k = threadIdx.x; k < NF; k += blockDim.x) { s.CR[k] = c.CR[k]; s.TV[k] = c.TV[k]; }
+  for (int k = threadIdx.x; k < NR; k += blockDim.x) { s.MUD[k] = c.MUD[k]; s.MUR[k] = c.MUR[k]; }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int grp = w / WPC, rk = w - grp * WPC;
+  double* W = s.W[w];
+  double* Pw = s.P[w];
+  double* LLg = s.LL[grp];
+  const bool own = lane < NR;
+  const int li = own ? lane : 0;
+  const uint32_t sk0 = (uint32_t)(r.seed & 0xffffffffull), sk1 = (uint32_t)(r.seed >> 32);
+  const double PDd = c.PD[li * NR + li], PRd = c.PR[li * NR + li];
+  // the chain loop is uniform over the workgroup (its barriers): groups past the last chain
+  // run a copy of the last one and store nothing
+  for (int base = blockIdx.x * CPG; base < r.n_chains; base += gridDim.x * CPG) {
+    const bool live = base + grp < r.n_chains;
+    if constexpr (WPC == 1) {          // no workgroup barriers: a wave past the end just leaves
+      if (!live) break;
+    }
+    const int chain = live ? base + grp : r.n_chains - 1;
+    const bool store = live && rk == 0;
+    double D = r.x0 ? r.x0[(size_t)chain * 2 * NR + li] : s.MUD[li];
+    double R = r.x0 ? r.x0[(size_t)chain * 2 * NR + NR + li] : s.MUR[li];
+    // prior gradients g = P (x - mu) (same FMA order as mh_chain_kernel)
+    W[lane] = own ? D - s.MUD[lane] : 0.0;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    double gD = 0.0;
+#pragma unroll 1
+    for (int k = 0; k < NR; ++k) gD = fma(c.PD[li * NR + k], W[k], gD);
+    __builtin_amdgcn_wave_barrier();
+    W[lane] = own ? R - s.MUR[lane] : 0.0;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    double gR = 0.0;
+#pragma unroll 1
+    for (int k = 0; k < NR; ++k) gR = fma(c.PR[li * NR + k], W[k], gR);
+    __builtin_amdgcn_wave_barrier();
+    // the state's per-ROI log-likelihoods: 48 evaluations
+#pragma unroll 1
+    for (int b = rk; b < NR / kQ; b += WPC) {
+      // lane q < kQ: ROI b kQ + q at the state
+      const int mi = b * kQ + (lane & (kQ - 1));
+      double out[kQ];
+      eval_batch(s, W, Pw, lane, mi, __shfl(D, mi), __shfl(R, mi), c.k2p, out);
+      double o = out[0];
+#pragma unroll
+      for (int q = 1; q < kQ; ++q) o = lane == q ? out[q] : o;
+      if (lane < kQ) LLg[b * kQ + lane] = o;
+    }
+    if constexpr (WPC > 1) __syncthreads();
+    else { __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); }
+    double ll = LLg[li];
+    if constexpr (WPC > 1) __syncthreads();
+    double sD = r.scaling, sR = r.scaling;
+    int aD = 0, aR = 0;
+    double accD = 0.0, accR = 0.0;
+    double mD = 0.0, m2D = 0.0, mR = 0.0, m2R = 0.0;
+    long long nk = 0;
+    const uint32_t ch_lo = (uint32_t)((unsigned long long)chain & 0xffffffffull);
+    const uint32_t ch_hi = (uint32_t)((unsigned long long)chain >> 32);
+    const int total = r.n_tune + r.n_draws;
+    double* Zw = W;                    // sweep draws in the wave's scratch: Z[96] LU[96] KEY[96] ORD[96]
+    double* LUw = W + 2 * NR;
+    uint32_t* KEYw = reinterpret_cast<uint32_t*>(W + 4 * NR);
+    int* ORDw = reinterpret_cast<int*>(W + 5 * NR);
+    for (int it = 0; it < total; ++it) {
+      if (it < r.n_tune && it > 0 && it % r.tune_interval == 0) {
+        sD = tune_scale(sD, (double)aD / r.tune_interval);
+        sR = tune_scale(sR, (double)aR / r.tune_interval);
+        aD = aR = 0;
+      }
+      if (MH_BEXP & 16) {                // diagnostic: identity order, no RNG
+        for (int h = 0; h < 2; ++h) {
+          const int k = lane + 64 * h;
+          if (k < 2 * NR) { Zw[k] = 0.5; LUw[k] = -1.0; ORDw[k] = k; }
+        }
+      } else
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = lane + 64 * h;
+        if (k < 2 * NR) {
+          uint32_t q[4] = {(uint32_t)k, (uint32_t)it, ch_lo, ch_hi};
+          philox(q, sk0, sk1);
+          const double u1 = ((double)q[0] + 1.0) * 2.3283064365386963e-10;
+          const double u2 = ((double)q[1] + 0.5) * 2.3283064365386963e-10;
+          Zw[k] = sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
+          LUw[k] = log(((double)q[2] + 0.5) * 2.3283064365386963e-10);
+          KEYw[k] = q[3];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      if (!(MH_BEXP & 16))
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = lane + 64 * h;
+        if (k < 2 * NR) {
+          const uint32_t kk = KEYw[k];
+          int rank = 0;
+#pragma unroll 8
+          for (int j = 0; j < 2 * NR; ++j) {
+            const uint32_t kj = KEYw[j];
+            rank += (kj < kk) | ((kj == kk) & (j < k));
+          }
+          ORDw[rank] = k;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      // to registers: lane i holds its ROI's two proposals / accept uniforms, lane j the order
+      const double dD = Zw[li] * sD, dR = Zw[NR + li] * sR;
+      const double luD = LUw[li], luR = LUw[NR + li];
+      const int ordA = ORDw[lane], ordB = ORDw[64 + (lane & 31)];
+      __builtin_amdgcn_wave_barrier();
+      const double pD = D + dD, pR = R + dR;
+      // the 144 evaluations, dealt to the chain's waves by batch
+#pragma unroll 1
+      for (int b = rk; b < kNE / kQ; b += WPC) {
+        // lane q < kQ: evaluation n = b kQ + q = 3 i + cc
+        const int n = b * kQ + (lane & (kQ - 1)), mi = n / 3, cc = n - 3 * mi;
+        const double sd = __shfl(D, mi), spd = __shfl(pD, mi), sr = __shfl(R, mi), spr = __shfl(pR, mi);
+        double out[kQ];
+        eval_batch(s, W, Pw, lane, mi, cc == 1 ? sd : spd, cc == 0 ? sr : spr, c.k2p, out);
+        double o = out[0];
+#pragma unroll
+        for (int q = 1; q < kQ; ++q) o = lane == q ? out[q] : o;
+        if (lane < kQ) LLg[b * kQ + lane] = o;
+      }
+      if constexpr (WPC > 1) __syncthreads();
+      else { __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); }
+      const double L0 = LLg[3 * li], L1 = LLg[3 * li + 1], L2 = LLg[3 * li + 2];
+      if constexpr (WPC > 1) __syncthreads();
+      // ---- the sweep: wave-uniform scan over the shuffled order.  An accept adds delta times
+      // column i of P to g (P is exactly symmetric, spd_inverse: column i = row i); the rows are
+      // loaded 4 elements ahead, so an accept never waits on L2.
+      double run = 0.0;
+      unsigned long long fD = 0ull, fR = 0ull;   // elements accepted so far in this sweep
+#define PETMH_ELEM(jj) ((jj) < 64 ? __builtin_amdgcn_readlane(ordA, (jj)) : __builtin_amdgcn_readlane(ordB, (jj)-64))
+#define PETMH_PROW(dst, jj)                                                                   \
+  {                                                                                           \
+    const int kk_ = PETMH_ELEM((jj) < 2 * NR ? (jj) : 0);                                     \
+    dst = kk_ >= NR ? c.PR[(kk_ - NR) * NR + li] : c.PD[kk_ * NR + li];                       \
+  }
+#define PETMH_STEP(jj, prw)                                                                   \
+  {                                                                                           \
+    const int k = PETMH_ELEM(jj);                                                             \
+    const int v = k >= NR, i = v ? k - NR : k;                                                \
+    const double delta = lane_bcast(v ? dR : dD, i);                                          \
+    const double gi = lane_bcast(v ? gR : gD, i);                                             \
+    const double pii = lane_bcast(v ? PRd : PDd, i);                                          \
+    const double lli = lane_bcast(ll, i);                                                     \
+    const bool oth = ((v ? fD : fR) >> i) & 1ull;                                             \
+    const double lln = lane_bcast(oth ? L2 : (v ? L1 : L0), i);                               \
+    const double lu = lane_bcast(v ? luR : luD, i);                                           \
+    const double dprior = -0.5 * (2.0 * delta * gi + delta * delta * pii);                    \
+    const double step = dprior + lln - lli;                                                   \
+    const double mr = r.vs_sweep_start ? run + step : step;                                   \
+    if (isfinite(mr) && lu < mr) { /* wave-uniform decision (metrop_select) */                \
+      run += step;                                                                            \
+      if (v) fR |= 1ull << i;                                                                 \
+      else fD |= 1ull << i;                                                                   \
+      if (lane == i) {                                                                        \
+        if (v == 0) { D = pD; aD += 1; if (it >= r.n_tune) accD += 1.0; }                     \
+        else { R = pR; aR += 1; if (it >= r.n_tune) accR += 1.0; }                            \
+        ll = lln;                                                                             \
+      }                                                                                       \
+      if (v == 0) gD = fma(delta, prw, gD);                                                   \
+      else gR = fma(delta, prw, gR);                                                          \
+    }                                                                                         \
+  }
+      if (!(MH_BEXP & 8)) {
+        double p0, p1, p2, p3;
+        PETMH_PROW(p0, 0) PETMH_PROW(p1, 1) PETMH_PROW(p2, 2) PETMH_PROW(p3, 3)
+#pragma unroll 1
+        for (int j = 0; j < 2 * NR; j += 4) {
+          PETMH_STEP(j, p0) PETMH_PROW(p0, j + 4)
+          PETMH_STEP(j + 1, p1) PETMH_PROW(p1, j + 5)
+          PETMH_STEP(j + 2, p2) PETMH_PROW(p2, j + 6)
+          PETMH_STEP(j + 3, p3) PETMH_PROW(p3, j + 7)
+        }
+      }
+#undef PETMH_STEP
+#undef PETMH_PROW
+#undef PETMH_ELEM
+      if (it >= r.n_tune) {
+        if (r.draws && own && store) {
+          double* dr = r.draws + ((size_t)chain * r.n_draws + (it - r.n_tune)) * 2 * NR;
+          dr[lane] = D;
+          dr[NR + lane] = R;
+        }
+        ++nk;
+        const double dd = D - mD;
+        mD += dd / (double)nk;
+        m2D = fma(dd, D - mD, m2D);
+        const double dr = R - mR;
+        mR += dr / (double)nk;
+        m2R = fma(dr, R - mR, m2R);
+      }
+    }
+    if (own && store) {
+      double* st = r.stats + (size_t)chain * 2 * NR * 3;
+      st[lane * 3 + 0] = (double)nk;
+      st[lane * 3 + 1] = mD;
+      st[lane * 3 + 2] = m2D;
+      st[(NR + lane) * 3 + 0] = (double)nk;
+      st[(NR + lane) * 3 + 1] = mR;
+      st[(NR + lane) * 3 + 2] = m2R;
+      if (r.accept) {
+        r.accept[(size_t)chain * 2 * NR + lane] = accD;
+        r.accept[(size_t)chain * 2 * NR + NR + lane] = accR;
+      }
+      if (r.last) {
+        r.last[(size_t)chain * 2 * NR + lane] = D;
+        r.last[(size_t)chain * 2 * NR + NR + lane] = R;
+      }
+    }
+  }
+}
+
 // Joint log density at n points (one wave per point).
 __global__ __launch_bounds__(kWaves * 64) void mh_logp_kernel(MHConst c, const double* x, int n, double* out) {
   __shared__ Lds s;
@@ -371,8 +735,46 @@ __global__ void srtm2_kernel(const double* M, const double* cr, const double* tv
   }
 }
 
+template <int WPC>
+static hipError_t launch_batched(const MHConst& c, const MHRun& r, hipStream_t st) {
+  constexpr int CPG = kBW / WPC;
+  int grid = (r.n_chains + CPG - 1) / CPG;
+  if (grid > 256 * 16) grid = 256 * 16;
+  hipLaunchKernelGGL(mh_chain_batched<WPC>, dim3(grid), dim3(kBW * 64), 0, st, c, r);
+  return hipGetLastError();
+}
+
+// Kernel choice: MHRun.kernel / .wpc (petmh_set_kernel), else the environment (PETMH_KERNEL=wave |
+// batched, PETMH_WPC; A/B scripts), else automatic: the batched kernel for up to 256 chains
+// (12 waves per chain: the reference's 4-chain protocol is latency bound), one update at a time
+// above (one wave per chain fills the chip; it issues fewer instructions per chain-step).
 hipError_t launch_mh_chains(const MHConst& c, const MHRun& r, hipStream_t st) {
   if (r.n_chains <= 0) return hipSuccess;
+  static const int kind_env = [] {
+    const char* e = getenv("PETMH_KERNEL");
+    return !e ? 0 : e[0] == 'w' ? 1 : e[0] == 'b' ? 2 : 0;
+  }();
+  static const int wpc_env = [] {
+    const char* e = getenv("PETMH_WPC");
+    return e ? atoi(e) : 0;
+  }();
+  int kind = r.kernel ? r.kernel : kind_env;
+  if (kind == 0) kind = r.n_chains <= 256 ? 2 : 1;
+  if (kind == 2) {
+    static_assert(kBW % 4 == 0 && kBW > 4, "waves per chain 1, 2, 4 or kBW");
+    int wpc = r.wpc ? r.wpc : wpc_env;
+    if (wpc <= 0) {
+      wpc = 1;
+      for (const int nx : {2, 4, kBW})
+        if ((long long)r.n_chains * nx <= 256LL * kBW) wpc = nx;
+    }
+    switch (wpc) {
+      case 1: return launch_batched<1>(c, r, st);
+      case 2: return launch_batched<2>(c, r, st);
+      case 4: return launch_batched<4>(c, r, st);
+      default: return launch_batched<kBW>(c, r, st);
+    }
+  }
   int grid = (r.n_chains + kWaves - 1) / kWaves;
   if (grid > 256 * 4) grid = 256 * 4;
   hipLaunchKernelGGL(mh_chain_kernel, dim3(grid), dim3(kWaves * 64), 0, st, c, r);

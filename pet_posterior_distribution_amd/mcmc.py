@@ -24,7 +24,7 @@ from .distributed import merge_stats
 
 class MetropolisSRTM2:
     def __init__(self, time_vector, tac_ref, k2p, y_obs, sigma_noise, mu_DVR, Cov_DVR, mu_R1, Cov_R1, device=None,
-                 tune_interval=100, scaling=1.0, vs_sweep_start=True):
+                 tune_interval=100, scaling=1.0, vs_sweep_start=True, kernel='auto', waves_per_chain=0):
         self.device = torch.device('cuda', device if device is not None else torch.cuda.current_device())
         arr = lambda a: np.ascontiguousarray(a, dtype=np.float64)   # noqa: E731
         self._keep = [arr(time_vector), arr(tac_ref), arr(y_obs), arr(sigma_noise), arr(mu_DVR), arr(Cov_DVR),
@@ -40,6 +40,18 @@ class MetropolisSRTM2:
         self._h = h
         _lib.check_mh(_lib.lib().petmh_set_sampler(h, int(tune_interval), float(scaling), int(bool(vs_sweep_start))),
                       'petmh_set_sampler')
+        self.set_kernel(kernel, waves_per_chain)
+
+    _KERNELS = {'auto': 0, 'update': 1, 'batched': 2}
+
+    def set_kernel(self, kernel='auto', waves_per_chain=0):
+        """GPU chain kernel (petmh_set_kernel): 'update' = one element update at a time, one wave per
+        chain; 'batched' = the sweep's 144 possible likelihoods evaluated up front by waves_per_chain
+        (1, 2, 4, 12; 0 = auto) waves, then a scan; 'auto' = batched for <= 256 chains."""
+        if kernel not in self._KERNELS:
+            raise ValueError(f'kernel must be one of {sorted(self._KERNELS)}')
+        _lib.check_mh(_lib.lib().petmh_set_kernel(self._h, self._KERNELS[kernel], int(waves_per_chain)),
+                      'petmh_set_kernel')
 
     def close(self):
         if getattr(self, '_h', None) is not None:

@@ -202,3 +202,47 @@ def test_mh_chain_rejects_nonfinite_proposals(g2):
     assert n_bad[0] > 0
     assert np.isfinite(res['last']).all()
     mh.close()
+
+
+def test_batched_kernel_invariant_to_waves_per_chain(g2):
+    """The batched sampler deals a chain's 144 proposal evaluations to 1, 2, 4 or 12 waves.  A chain's
+    path depends only on its index: stats, last state, trace and acceptance are bitwise identical
+    for every waves-per-chain setting and chain count."""
+    from pet_posterior_distribution_amd.mcmc import MetropolisSRTM2
+    P = make_problem(g2, case=2, noise=0.06, seed=9)
+    mh = MetropolisSRTM2(**P)
+    ref = None
+    for wpc, n in ((12, 40), (4, 700), (2, 1500), (1, 4000), (1, 40)):
+        mh.set_kernel('batched', wpc)
+        res = mh.run(n, 4, 3, seed=77, return_chains=True, return_draws=True)
+        got = (res['chain_stats'][:40], res['last'][:40], res['draws'][:40].cpu().numpy(),
+               res['accept_rate'][:40])
+        if ref is None:
+            ref = got
+            continue
+        for a, b in zip(got, ref):
+            np.testing.assert_array_equal(a, b)
+    mh.close()
+
+
+@pytest.mark.parametrize('vs0', [True, False])
+def test_batched_and_update_kernels_same_chain_path(g2, vs0):
+    """The batched kernel (likelihoods of every possible proposal state up front, then a scan) and the
+    one-update-at-a-time kernel take the same accept/reject path: they differ only in the order of
+    the 54-frame sum, so a decision within ~1e-12 of its threshold may flip (allow one chain)."""
+    from pet_posterior_distribution_amd.mcmc import MetropolisSRTM2
+    P = make_problem(g2, case=3, noise=0.08, seed=4)
+    mh = MetropolisSRTM2(**P, vs_sweep_start=vs0)
+    out = {}
+    for k in ('update', 'batched'):
+        mh.set_kernel(k)
+        out[k] = mh.run(64, 30, 130, seed=2024, return_chains=True)
+    a, b = out['update'], out['batched']
+    same = np.all(np.abs(a['last'] - b['last']) <= 1e-9 * np.abs(b['last']), axis=1)
+    assert same.sum() >= 63, f'{64 - same.sum()} chains diverged between the kernels'
+    np.testing.assert_allclose(a['chain_stats'][same][..., 1], b['chain_stats'][same][..., 1], rtol=1e-9)
+    np.testing.assert_allclose(a['chain_stats'][same][..., 2], b['chain_stats'][same][..., 2], rtol=1e-6,
+                               atol=1e-12)
+    with pytest.raises(ValueError):
+        mh.set_kernel('batched', 3)
+    mh.close()
