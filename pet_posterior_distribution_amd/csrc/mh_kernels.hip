@@ -349,30 +349,45 @@ __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun 
 #ifndef MH_BEXP
 #define MH_BEXP 0
 #endif
+// scan: 0 = branch-free state updates, 1 = updates behind a branch on the decision (faster: 0.67
+// vs 0.74 us per element at 4 chains, profiles/r02/mh)
+#ifndef MH_SCAN_BRANCH
+#define MH_SCAN_BRANCH 1
+#endif
 #ifndef MH_P_UNROLL
 #define MH_P_UNROLL 1
 #endif
-constexpr int kQ = 8;                 // evaluations per batch
+#ifndef MH_Q
+#define MH_Q 4
+#endif
+constexpr int kQ = MH_Q;              // evaluations per batch (144 = 36 batches of 4: 3 per wave at 12 waves)
+static_assert(kQ == 4 || kQ == 8, "frame-sum lane groups of 16 or 8");
 #ifndef MH_BW
 #define MH_BW 12
 #endif
 constexpr int kBW = MH_BW;            // waves per workgroup
 constexpr int kNE = 3 * NR;           // evaluations per draw
+// per-wave scratch (doubles): the batch's e rows / frame terms, or the sweep draws Z[96] LU[96]
+// KEY[96] (u32) ORD[96] (i32)
+constexpr int kWD = kQ * 64 > 6 * NR ? kQ * 64 : 6 * NR;
+static_assert(kQ * MLD <= kWD && kQ * 64 <= kWD && 6 * NR <= kWD, "per-wave scratch");
 
 struct LdsB {
   double M[NF * MLD];
+  double PD[NR * NR], PR[NR * NR];    // prior precisions (the sweep's prior-gradient updates)
   double Y[NR * NF], SIG[NR * NF];
   double CR[NF], TV[NF];
   double MUD[NR], MUR[NR];
-  double W[kBW][kQ * 64];             // per wave: e rows [q][MLD] / frame terms [q][64] / sweep draws
+  double W[kBW][kWD];                 // per wave: e rows [q][MLD] / frame terms [q][64] / sweep draws
   double P[kBW][kQ * 4];              // per wave: the batch's (R1, k2, k2a, roi)
   double LL[kBW][kNE];                // per chain group: the draw's evaluations
+  double SH[kBW / 2][4 * NR];         // waves_per_chain > 1: the leader's D, R, D', R' per draw
 };
 
 // kQ log-likelihoods.  Lane q < kQ brings evaluation q's (roi, DVR, R1) in (my_roi, my_dvr,
 // my_r1); the results come back wave-uniform in out[q].  W / P: this wave's scratch.
-// mcmc.py:151-155 per frame; the 54-frame sum is a stride-8 partial per lane plus a 3-step DPP
-// tree inside each 8-lane group (lane 8 q + 7 ends with evaluation q).  The transcendental part
+// mcmc.py:151-155 per frame; the 54-frame sum is a strided partial per lane plus a DPP tree
+// inside each group of 64 / kQ lanes (the group's last lane ends with its evaluation).  The transcendental part
 // runs one evaluation at a time (not unrolled: the fp64 exp / log / erfc constants would
 // otherwise be hoisted into registers kQ times over); the operator FMAs run kQ chains at once.
 __device__ __forceinline__ void eval_batch(const LdsB& s, double* W, double* P, int lane, int my_roi, double my_dvr,
@@ -446,16 +461,18 @@ __device__ __forceinline__ void eval_batch(const LdsB& s, double* W, double* P, 
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  const int qq = lane >> 3, pp = lane & 7;
+  constexpr int G = 64 / kQ;            // lanes per evaluation
+  const int qq = lane / G, pp = lane % G;
   double sum = 0.0;
 #pragma unroll
-  for (int m = 0; m < 8; ++m) sum += W[qq * 64 + pp + 8 * m];
+  for (int m = 0; m < kQ; ++m) sum += W[qq * 64 + pp + G * m];
   sum += dpp_f64<0x111>(sum);          // row_shr:1
   sum += dpp_f64<0x112>(sum);          // row_shr:2
   sum += dpp_f64<0x114>(sum);          // row_shr:4 -> lanes 7 / 15 of each row: their 8-lane group
+  if constexpr (G == 16) sum += dpp_f64<0x118>(sum);   // row_shr:8 -> lane 15: the row
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
-  for (int q = 0; q < kQ; ++q) out[q] = lane_bcast(sum, 8 * q + 7);
+  for (int q = 0; q < kQ; ++q) out[q] = lane_bcast(sum, G * q + G - 1);
 }
 
 template <int WPC>
@@ -467,6 +484,7 @@ __global__ __launch_bounds__(kBW * 64) void mh_chain_batched(MHConst c, MHRun r)
     s.M[k] = g < NF ? c.M[g * NF + f] : 0.0;   // global operator is [g][f]
   }
   for (int k = threadIdx.x; k < NR * NF; k += blockDim.x) { s.Y[k] = c.Y[k]; s.SIG[k] = c.SIG[k]; }
+  for (int k = threadIdx.x; k < NR * NR; k += blockDim.x) { s.PD[k] = c.PD[k]; s.PR[k] = c.PR[k]; }
   for (int k = threadIdx.x; k < NF; k += blockDim.x) { s.CR[k] = c.CR[k]; s.TV[k] = c.TV[k]; }
   for (int k = threadIdx.x; k < NR; k += blockDim.x) { s.MUD[k] = c.MUD[k]; s.MUR[k] = c.MUR[k]; }
   __syncthreads();
@@ -478,7 +496,7 @@ __global__ __launch_bounds__(kBW * 64) void mh_chain_batched(MHConst c, MHRun r)
   const bool own = lane < NR;
   const int li = own ? lane : 0;
   const uint32_t sk0 = (uint32_t)(r.seed & 0xffffffffull), sk1 = (uint32_t)(r.seed >> 32);
-  const double PDd = c.PD[li * NR + li], PRd = c.PR[li * NR + li];
+  const double PDd = s.PD[li * NR + li], PRd = s.PR[li * NR + li];
   // the chain loop is uniform over the workgroup (its barriers): groups past the last chain
   // run a copy of the last one and store nothing
   for (int base = blockIdx.x * CPG; base < r.n_chains; base += gridDim.x * CPG) {
@@ -496,14 +514,14 @@ __global__ __launch_bounds__(kBW * 64) void mh_chain_batched(MHConst c, MHRun r)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     double gD = 0.0;
 #pragma unroll 1
-    for (int k = 0; k < NR; ++k) gD = fma(c.PD[li * NR + k], W[k], gD);
+    for (int k = 0; k < NR; ++k) gD = fma(s.PD[li * NR + k], W[k], gD);
     __builtin_amdgcn_wave_barrier();
     W[lane] = own ? R - s.MUR[lane] : 0.0;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     double gR = 0.0;
 #pragma unroll 1
-    for (int k = 0; k < NR; ++k) gR = fma(c.PR[li * NR + k], W[k], gR);
+    for (int k = 0; k < NR; ++k) gR = fma(s.PR[li * NR + k], W[k], gR);
     __builtin_amdgcn_wave_barrier();
     // the state's per-ROI log-likelihoods: 48 evaluations
 #pragma unroll 1
@@ -533,56 +551,83 @@ __global__ __launch_bounds__(kBW * 64) void mh_chain_batched(MHConst c, MHRun r)
     double* LUw = W + 2 * NR;
     uint32_t* KEYw = reinterpret_cast<uint32_t*>(W + 4 * NR);
     int* ORDw = reinterpret_cast<int*>(W + 5 * NR);
+    // waves_per_chain > 1: the group's first wave (the leader) alone tunes, draws the sweep's random
+    // numbers, scans and keeps the statistics; it hands D, R and the proposals to the others
+    // through LDS once per draw (a redundant scan in every wave would triple its issue cost)
+    const bool lead = WPC == 1 || rk == 0;
     for (int it = 0; it < total; ++it) {
-      if (it < r.n_tune && it > 0 && it % r.tune_interval == 0) {
-        sD = tune_scale(sD, (double)aD / r.tune_interval);
-        sR = tune_scale(sR, (double)aR / r.tune_interval);
-        aD = aR = 0;
-      }
-      if (MH_BEXP & 16) {                // diagnostic: identity order, no RNG
+      double dD = 0.0, dR = 0.0, luD = 0.0, luR = 0.0;
+      int ordA = 0, ordB = 0;
+      if (lead) {
+        if (it < r.n_tune && it > 0 && it % r.tune_interval == 0) {
+          sD = tune_scale(sD, (double)aD / r.tune_interval);
+          sR = tune_scale(sR, (double)aR / r.tune_interval);
+          aD = aR = 0;
+        }
+        if (MH_BEXP & 16) {                // diagnostic: identity order, no RNG
+          for (int h = 0; h < 2; ++h) {
+            const int k = lane + 64 * h;
+            if (k < 2 * NR) { Zw[k] = 0.5; LUw[k] = -1.0; ORDw[k] = k; }
+          }
+        } else
+#pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int k = lane + 64 * h;
-          if (k < 2 * NR) { Zw[k] = 0.5; LUw[k] = -1.0; ORDw[k] = k; }
-        }
-      } else
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int k = lane + 64 * h;
-        if (k < 2 * NR) {
-          uint32_t q[4] = {(uint32_t)k, (uint32_t)it, ch_lo, ch_hi};
-          philox(q, sk0, sk1);
-          const double u1 = ((double)q[0] + 1.0) * 2.3283064365386963e-10;
-          const double u2 = ((double)q[1] + 0.5) * 2.3283064365386963e-10;
-          Zw[k] = sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
-          LUw[k] = log(((double)q[2] + 0.5) * 2.3283064365386963e-10);
-          KEYw[k] = q[3];
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      if (!(MH_BEXP & 16))
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int k = lane + 64 * h;
-        if (k < 2 * NR) {
-          const uint32_t kk = KEYw[k];
-          int rank = 0;
-#pragma unroll 8
-          for (int j = 0; j < 2 * NR; ++j) {
-            const uint32_t kj = KEYw[j];
-            rank += (kj < kk) | ((kj == kk) & (j < k));
+          if (k < 2 * NR) {
+            uint32_t q[4] = {(uint32_t)k, (uint32_t)it, ch_lo, ch_hi};
+            philox(q, sk0, sk1);
+            const double u1 = ((double)q[0] + 1.0) * 2.3283064365386963e-10;
+            const double u2 = ((double)q[1] + 0.5) * 2.3283064365386963e-10;
+            Zw[k] = sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
+            LUw[k] = log(((double)q[2] + 0.5) * 2.3283064365386963e-10);
+            KEYw[k] = q[3];
           }
-          ORDw[rank] = k;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        if (!(MH_BEXP & 16))
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int k = lane + 64 * h;
+          if (k < 2 * NR) {
+            const uint32_t kk = KEYw[k];
+            int rank = 0;
+#pragma unroll 8
+            for (int j = 0; j < 2 * NR; ++j) {
+              const uint32_t kj = KEYw[j];
+              rank += (kj < kk) | ((kj == kk) & (j < k));
+            }
+            ORDw[rank] = k;
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        // to registers: lane i holds its ROI's two proposals / accept uniforms, lane j the order
+        dD = Zw[li] * sD;
+        dR = Zw[NR + li] * sR;
+        luD = LUw[li];
+        luR = LUw[NR + li];
+        ordA = ORDw[lane];
+        ordB = ORDw[64 + (lane & 31)];
+        __builtin_amdgcn_wave_barrier();
+      }
+      double pD = D + dD, pR = R + dR;
+      if constexpr (WPC > 1) {
+        double* SHg = s.SH[grp];
+        if (lead && own) {
+          SHg[lane] = D;
+          SHg[NR + lane] = R;
+          SHg[2 * NR + lane] = pD;
+          SHg[3 * NR + lane] = pR;
+        }
+        __syncthreads();
+        if (!lead) {
+          D = SHg[li];
+          R = SHg[NR + li];
+          pD = SHg[2 * NR + li];
+          pR = SHg[3 * NR + li];
         }
       }
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      // to registers: lane i holds its ROI's two proposals / accept uniforms, lane j the order
-      const double dD = Zw[li] * sD, dR = Zw[NR + li] * sR;
-      const double luD = LUw[li], luR = LUw[NR + li];
-      const int ordA = ORDw[lane], ordB = ORDw[64 + (lane & 31)];
-      __builtin_amdgcn_wave_barrier();
-      const double pD = D + dD, pR = R + dR;
       // the 144 evaluations, dealt to the chain's waves by batch
 #pragma unroll 1
       for (int b = rk; b < kNE / kQ; b += WPC) {
@@ -598,61 +643,90 @@ __global__ __launch_bounds__(kBW * 64) void mh_chain_batched(MHConst c, MHRun r)
       }
       if constexpr (WPC > 1) __syncthreads();
       else { __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); }
-      const double L0 = LLg[3 * li], L1 = LLg[3 * li + 1], L2 = LLg[3 * li + 2];
-      if constexpr (WPC > 1) __syncthreads();
+      // (the leader reads LLg below; the others next write it after the next draw's hand-off
+      // barrier, which the leader joins only after its scan)
       // ---- the sweep: wave-uniform scan over the shuffled order.  An accept adds delta times
-      // column i of P to g (P is exactly symmetric, spd_inverse: column i = row i); the rows are
-      // loaded 4 elements ahead, so an accept never waits on L2.
+      // column i of P to g (P is exactly symmetric, spd_inverse: column i = row i, read from LDS).
       double run = 0.0;
       unsigned long long fD = 0ull, fR = 0ull;   // elements accepted so far in this sweep
-#define PETMH_ELEM(jj) ((jj) < 64 ? __builtin_amdgcn_readlane(ordA, (jj)) : __builtin_amdgcn_readlane(ordB, (jj)-64))
-#define PETMH_PROW(dst, jj)                                                                   \
+      // scan-order tables: lane j holds element ORD[j]'s (ORD[64 + j]'s in the *B set) proposal
+      // step, P_ii, log accept uniform and its two candidate likelihoods (the other element of
+      // its ROI not accepted / accepted), so a step broadcasts them by its own index j and only
+      // g_i and ll_i wait on the previous decisions
+#define PETMH_TAB(ordX, kX, dlX, piX, uX, lnX, lyX)                                            \
+  const int kX = ordX;                                                                        \
+  double dlX, piX, uX, lnX, lyX;                                                              \
   {                                                                                           \
-    const int kk_ = PETMH_ELEM((jj) < 2 * NR ? (jj) : 0);                                     \
-    dst = kk_ >= NR ? c.PR[(kk_ - NR) * NR + li] : c.PD[kk_ * NR + li];                       \
+    const bool v_ = kX >= NR;                                                                 \
+    const int i_ = v_ ? kX - NR : kX;                                                         \
+    const double dd_ = __shfl(dD, i_), dr_ = __shfl(dR, i_);                                  \
+    const double pd_ = __shfl(PDd, i_), pr_ = __shfl(PRd, i_);                                \
+    const double ud_ = __shfl(luD, i_), ur_ = __shfl(luR, i_);                                \
+    dlX = v_ ? dr_ : dd_;                                                                     \
+    piX = v_ ? pr_ : pd_;                                                                     \
+    uX = v_ ? ur_ : ud_;                                                                      \
+    lnX = LLg[3 * i_ + (v_ ? 1 : 0)];                                                         \
+    lyX = LLg[3 * i_ + 2];                                                                    \
   }
-#define PETMH_STEP(jj, prw)                                                                   \
+      PETMH_TAB(ordA, kA, dlA, piA, uA, lnA, lyA)
+      PETMH_TAB(ordB, kB, dlB, piB, uB, lnB, lyB)
+#undef PETMH_TAB
+// one element of the sweep; the state updates sit behind the (wave-uniform) decision
+#define PETMH_STEP(jl, kX, dlX, piX, uX, lnX, lyX)                                             \
   {                                                                                           \
-    const int k = PETMH_ELEM(jj);                                                             \
-    const int v = k >= NR, i = v ? k - NR : k;                                                \
-    const double delta = lane_bcast(v ? dR : dD, i);                                          \
+    const int k = __builtin_amdgcn_readlane(kX, (jl));                                        \
+    const bool v = k >= NR;                                                                   \
+    const int i = v ? k - NR : k;                                                             \
+    const double prw = (v ? s.PR : s.PD)[i * NR + li];   /* column i = row i (P symmetric) */ \
+    const double delta = lane_bcast(dlX, (jl));                                               \
+    const double pii = lane_bcast(piX, (jl));                                                 \
+    const double lu = lane_bcast(uX, (jl));                                                   \
+    const double lno = lane_bcast(lnX, (jl)), lyes = lane_bcast(lyX, (jl));                   \
     const double gi = lane_bcast(v ? gR : gD, i);                                             \
-    const double pii = lane_bcast(v ? PRd : PDd, i);                                          \
     const double lli = lane_bcast(ll, i);                                                     \
     const bool oth = ((v ? fD : fR) >> i) & 1ull;                                             \
-    const double lln = lane_bcast(oth ? L2 : (v ? L1 : L0), i);                               \
-    const double lu = lane_bcast(v ? luR : luD, i);                                           \
+    const double lln = oth ? lyes : lno;                                                      \
     const double dprior = -0.5 * (2.0 * delta * gi + delta * delta * pii);                    \
     const double step = dprior + lln - lli;                                                   \
     const double mr = r.vs_sweep_start ? run + step : step;                                   \
-    if (isfinite(mr) && lu < mr) { /* wave-uniform decision (metrop_select) */                \
-      run += step;                                                                            \
-      if (v) fR |= 1ull << i;                                                                 \
-      else fD |= 1ull << i;                                                                   \
-      if (lane == i) {                                                                        \
-        if (v == 0) { D = pD; aD += 1; if (it >= r.n_tune) accD += 1.0; }                     \
-        else { R = pR; aR += 1; if (it >= r.n_tune) accR += 1.0; }                            \
-        ll = lln;                                                                             \
-      }                                                                                       \
-      if (v == 0) gD = fma(delta, prw, gD);                                                   \
-      else gR = fma(delta, prw, gR);                                                          \
+    const bool acc = isfinite(mr) && lu < mr; /* wave-uniform decision (metrop_select) */     \
+    if (!MH_SCAN_BRANCH || acc) {                                                             \
+      run = acc ? run + step : run;                                                           \
+      const unsigned long long bit = acc ? 1ull << i : 0ull;                                  \
+      fR |= v ? bit : 0ull;                                                                   \
+      fD |= v ? 0ull : bit;                                                                   \
+      const bool mine = acc && lane == i;                                                     \
+      D = (mine && !v) ? pD : D;                                                              \
+      R = (mine && v) ? pR : R;                                                               \
+      ll = mine ? lln : ll;                                                                   \
+      aD += (mine && !v) ? 1 : 0;                                                             \
+      aR += (mine && v) ? 1 : 0;                                                              \
+      accD += (mine && !v && kept) ? 1.0 : 0.0;                                               \
+      accR += (mine && v && kept) ? 1.0 : 0.0;                                                \
+      /* fma(0, finite row, g) == g: the unselected g is unchanged */                          \
+      gD = fma((acc && !v) ? delta : 0.0, prw, gD);                                           \
+      gR = fma((acc && v) ? delta : 0.0, prw, gR);                                            \
     }                                                                                         \
   }
-      if (!(MH_BEXP & 8)) {
-        double p0, p1, p2, p3;
-        PETMH_PROW(p0, 0) PETMH_PROW(p1, 1) PETMH_PROW(p2, 2) PETMH_PROW(p3, 3)
+      if (lead && !(MH_BEXP & 8)) {
+        const bool kept = it >= r.n_tune;
 #pragma unroll 1
-        for (int j = 0; j < 2 * NR; j += 4) {
-          PETMH_STEP(j, p0) PETMH_PROW(p0, j + 4)
-          PETMH_STEP(j + 1, p1) PETMH_PROW(p1, j + 5)
-          PETMH_STEP(j + 2, p2) PETMH_PROW(p2, j + 6)
-          PETMH_STEP(j + 3, p3) PETMH_PROW(p3, j + 7)
+        for (int j = 0; j < 64; j += 4) {
+          PETMH_STEP(j, kA, dlA, piA, uA, lnA, lyA)
+          PETMH_STEP(j + 1, kA, dlA, piA, uA, lnA, lyA)
+          PETMH_STEP(j + 2, kA, dlA, piA, uA, lnA, lyA)
+          PETMH_STEP(j + 3, kA, dlA, piA, uA, lnA, lyA)
+        }
+#pragma unroll 1
+        for (int j = 0; j < 2 * NR - 64; j += 4) {
+          PETMH_STEP(j, kB, dlB, piB, uB, lnB, lyB)
+          PETMH_STEP(j + 1, kB, dlB, piB, uB, lnB, lyB)
+          PETMH_STEP(j + 2, kB, dlB, piB, uB, lnB, lyB)
+          PETMH_STEP(j + 3, kB, dlB, piB, uB, lnB, lyB)
         }
       }
 #undef PETMH_STEP
-#undef PETMH_PROW
-#undef PETMH_ELEM
-      if (it >= r.n_tune) {
+      if (lead && it >= r.n_tune) {
         if (r.draws && own && store) {
           double* dr = r.draws + ((size_t)chain * r.n_draws + (it - r.n_tune)) * 2 * NR;
           dr[lane] = D;
