@@ -354,6 +354,10 @@ __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun 
 #ifndef MH_SCAN_BRANCH
 #define MH_SCAN_BRANCH 1
 #endif
+// per-frame transcendental loop: evaluations in flight per wave
+#ifndef MH_T_UNROLL
+#define MH_T_UNROLL 1
+#endif
 #ifndef MH_P_UNROLL
 #define MH_P_UNROLL 1
 #endif
@@ -433,7 +437,7 @@ __device__ __forceinline__ void eval_batch(const LdsB& s, double* W, double* P, 
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   const double crf = s.CR[f];
-#pragma unroll 1
+#pragma unroll MH_T_UNROLL
   for (int q = 0; q < kQ; ++q) {
     double l = 0.0;
     if (lane < NF) {
