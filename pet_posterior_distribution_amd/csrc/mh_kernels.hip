@@ -8,6 +8,7 @@
 // proposal costs one 54 x 54 operator application + 54 truncated-normal terms;
 // the MvNormal prior change is 2 d g_i + d^2 P_ii (g kept current on accept).
 #include "mh_internal.h"
+#include "logphi_coef.h"
 
 #include <cstdlib>
 
@@ -19,9 +20,66 @@
 #define MH_MV_UNROLL 28   // operator-row matvec: 16-B steps unrolled
 #endif
 
+// log Phi of the truncated-normal normaliser: 1 = the piecewise polynomial of logphi_coef.h
+// (scripts/gen_logphi.py; |err| <= 1.2e-16 on [0, 10)), 0 = ocml log(erfc) (A/B)
+#ifndef MH_LOGPHI_POLY
+#define MH_LOGPHI_POLY 1
+#endif
+
 namespace petmh {
 
 constexpr int NR = kNRoi, NF = kNFrames;
+constexpr int LPNI = PETMH_LOGPHI_NI, LPLD = 18;   // LDS row: 16 coefficients (c15 = 0) + 2 pad doubles,
+static_assert(PETMH_LOGPHI_DEG == 14, "8 x 16-B pieces per row");   // 144-B rows: conflict-free ds_read_b128
+__constant__ double c_logphi[LPNI][PETMH_LOGPHI_DEG + 1] = PETMH_LOGPHI_COEF;
+
+// log Phi(x) for 0 <= x < 10 (x = NaN: NaN): interval k = floor(x), Horner in u = x - (k + 0.5)
+// from the LDS copy of the coefficients (row k: pieces (c_2j, c_2j+1)).
+__device__ __forceinline__ double log_phi_poly(const double* tab, double x) {
+  int k = (int)x;
+  k = k < 0 ? 0 : (k > LPNI - 1 ? LPNI - 1 : k);
+  const double u = x - ((double)k + 0.5);
+  const double2* row = reinterpret_cast<const double2*>(tab + k * LPLD);
+  double p = row[7].x;
+#pragma unroll
+  for (int j = 6; j >= 0; --j) {
+    const double2 cc = row[j];
+    p = fma(p, u, cc.y);
+    p = fma(p, u, cc.x);
+  }
+  return p;
+}
+
+// log of the noise scale sigma > 0 (MH_FAST_LOG): frexp to m in [1/sqrt 2, sqrt 2), f = m - 1,
+// s = f / (2 + f), log m = f - (f^2/2 - s (f^2/2 + R(s^2))) with R the degree-7 minimax of
+// fdlibm's e_log.c (Lg1..Lg7), k ln 2 in two parts: <= 1 ulp (checked against numpy / mpmath).
+// About a fifth of ocml's instruction count.  Zero, negative, inf and NaN go to ocml's log.
+#ifndef MH_FAST_LOG
+#define MH_FAST_LOG 1
+#endif
+__device__ __forceinline__ double log_pos(double x) {
+  if (!(x > 0.0 && x < __builtin_huge_val())) return log(x);
+  int e;
+  double m = frexp(x, &e);
+  if (m < 0.70710678118654752440) {
+    m *= 2.0;
+    e -= 1;
+  }
+  const double f = m - 1.0, s = f / (2.0 + f), z = s * s, w = z * z;
+  const double t1 = w * (3.999999999940941908e-01 + w * (2.222219843214978396e-01 + w * 1.531383769920937332e-01));
+  const double t2 = z * (6.666666666666735130e-01 +
+                         w * (2.857142874366239149e-01 + w * (1.818357216161805012e-01 + w * 1.479819860511658591e-01)));
+  const double R = t2 + t1, hfsq = 0.5 * f * f, k = (double)e;
+  return k * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + k * 1.90821492927058770002e-10)) - f);
+}
+
+// LDS copy of the coefficient table (one element per thread)
+__device__ __forceinline__ void load_logphi(double* tab) {
+  for (int e = threadIdx.x; e < LPNI * LPLD; e += blockDim.x) {
+    const int k = e / LPLD, j = e - k * LPLD;
+    tab[e] = j <= PETMH_LOGPHI_DEG ? c_logphi[k][j] : 0.0;
+  }
+}
 #ifndef MH_WAVES
 #define MH_WAVES 8
 #endif
@@ -35,6 +93,7 @@ struct Lds {
   double Y[NR * NF], SIG[NR * NF];    // observed TAC / dt and noise sigma, [roi][frame]
   double CR[NF], TV[NF];
   double MUD[NR], MUR[NR];
+  alignas(16) double LPHI[LPNI * LPLD];   // log Phi polynomial (16-B aligned rows)
   double E[kWaves][64];               // per-wave exponential scratch
   double Z[kWaves][2 * NR];           // per-wave sweep draws: N(0,1) proposal per element
   double LU[kWaves][2 * NR];          //   log accept-uniform per element
@@ -135,12 +194,12 @@ __device__ __forceinline__ double roi_loglik(const Lds& s, double* e, int lane, 
 #if MH_EXP_MODE & 4
     const double lnd = 0.0;
 #else
-    const double lnd = xs < 10.0 ? log_ndtr(xs) : 0.0;
+    const double lnd = xs < 10.0 ? (MH_LOGPHI_POLY ? log_phi_poly(s.LPHI, xs) : log_ndtr(xs)) : 0.0;
 #endif
 #if MH_EXP_MODE & 2
     l = -0.5 * z * z - 0.9189385332046727 - sig - lnd;
 #else
-    l = -0.5 * z * z - 0.9189385332046727 - log(sig) - lnd;
+    l = -0.5 * z * z - 0.9189385332046727 - (MH_FAST_LOG ? log_pos(sig) : log(sig)) - lnd;
 #endif
   }
   __builtin_amdgcn_wave_barrier();
@@ -156,6 +215,7 @@ __device__ void load_lds(Lds& s, const MHConst& c) {
   for (int k = threadIdx.x; k < NR * NF; k += blockDim.x) { s.Y[k] = c.Y[k]; s.SIG[k] = c.SIG[k]; }
   for (int k = threadIdx.x; k < NF; k += blockDim.x) { s.CR[k] = c.CR[k]; s.TV[k] = c.TV[k]; }
   for (int k = threadIdx.x; k < NR; k += blockDim.x) { s.MUD[k] = c.MUD[k]; s.MUR[k] = c.MUR[k]; }
+  load_logphi(s.LPHI);
   __syncthreads();
 }
 
@@ -382,6 +442,7 @@ struct LdsB {
   double Y[NR * NF], SIG[NR * NF];
   double CR[NF], TV[NF];
   double MUD[NR], MUR[NR];
+  alignas(16) double LPHI[LPNI * LPLD];   // log Phi polynomial (16-B aligned rows)
   double W[kBW][kWD];                 // per wave: e rows [q][MLD] / frame terms [q][64] / sweep draws
   double P[kBW][kQ * 4];              // per wave: the batch's (R1, k2, k2a, roi)
   double LL[kBW][kNE];                // per chain group: the draw's evaluations
@@ -457,8 +518,9 @@ __device__ __forceinline__ void eval_batch(const LdsB& s, double* W, double* P, 
       const double xs = sn * inv;
       // log Phi(xs) (log_ndtr): xs = sqrt(sn) / SIG >= 0 or NaN, so only its x > -1 branch
       // log(erfc(-x / sqrt 2) / 2) is reachable (NaN falls through to NaN either way)
-      const double lnd = xs < 10.0 ? log(0.5 * erfc(-xs * 0.7071067811865476)) : 0.0;
-      l = -0.5 * z * z - 0.9189385332046727 - log(sig) - lnd;
+      const double lnd = xs < 10.0 ? (MH_LOGPHI_POLY ? log_phi_poly(s.LPHI, xs)
+                                                      : log(0.5 * erfc(-xs * 0.7071067811865476))) : 0.0;
+      l = -0.5 * z * z - 0.9189385332046727 - (MH_FAST_LOG ? log_pos(sig) : log(sig)) - lnd;
 #endif
     }
     W[q * 64 + lane] = l;
@@ -491,6 +553,7 @@ __global__ __launch_bounds__(kBW * 64) void mh_chain_batched(MHConst c, MHRun r)
   for (int k = threadIdx.x; k < NR * NR; k += blockDim.x) { s.PD[k] = c.PD[k]; s.PR[k] = c.PR[k]; }
   for (int k = threadIdx.x; k < NF; k += blockDim.x) { s.CR[k] = c.CR[k]; s.TV[k] = c.TV[k]; }
   for (int k = threadIdx.x; k < NR; k += blockDim.x) { s.MUD[k] = c.MUD[k]; s.MUR[k] = c.MUR[k]; }
+  load_logphi(s.LPHI);
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int grp = w / WPC, rk = w - grp * WPC;

@@ -72,3 +72,32 @@ def test_c_sampler_thread_invariance(g2, cmh):
     b = prob.run(6, 20, 30, 99, threads=4)
     for u, v in zip(a, b):
         np.testing.assert_array_equal(u, v)
+
+
+def test_logphi_polynomial_vs_scipy():
+    """The MH kernels' log Phi (csrc/logphi_coef.h, scripts/gen_logphi.py): piecewise degree-14
+    polynomials on [0, 10), evaluated by Horner as the kernel does, against scipy.special.log_ndtr
+    (the reference's TruncatedNormal normaliser, mcmc.py:151-155) on a dense grid (<= 1.5e-15: scipy's
+    own error) and against the exact function (mpmath, 30 digits) on every 40th point (<= 2.5e-16;
+    the values' own fp64 rounding is 1.1e-16 at x = 0)."""
+    import re
+    from scipy.special import log_ndtr
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            'pet_posterior_distribution_amd', 'csrc', 'logphi_coef.h')).read()
+    rows = re.findall(r'\{([^{}]+)\}', hdr[hdr.index('PETMH_LOGPHI_COEF'):])
+    tab = np.array([[float(v) for v in r.split(',')] for r in rows])
+    assert tab.shape == (10, 15)
+    x = np.concatenate([np.linspace(0.0, 10.0, 200001)[:-1], [1e-300, 0.5, 9.999999999]])
+    k = np.clip(x.astype(np.int64), 0, 9)
+    u = x - (k + 0.5)
+    p = np.zeros_like(x)
+    for j in range(14, -1, -1):
+        p = p * u + tab[k, j]
+    err = np.abs(p - log_ndtr(x))          # scipy itself is off by up to ~9e-16 near x = 0
+    assert err.max() <= 1.5e-15, (err.max(), x[err.argmax()])
+    import mpmath as mp
+    mp.mp.dps = 30
+    xs = x[::40]
+    exact = np.array([float(mp.log(mp.ncdf(mp.mpf(float(v))))) for v in xs])
+    e2 = np.abs(p[::40] - exact)
+    assert e2.max() <= 2.5e-16, (e2.max(), xs[e2.argmax()])
