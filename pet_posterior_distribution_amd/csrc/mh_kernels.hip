@@ -153,7 +153,13 @@ __device__ __forceinline__ double log_ndtr(double x) {
 
 // Sum over frames of the TruncatedNormal(lower=0) log density of ROI i with
 // parameters (DVR, R1); every lane returns the total (mcmc.py:151-155).
-__device__ __forceinline__ double roi_loglik(const Lds& s, double* e, int lane, int i, double dvr, double r1, double k2p) {
+// MH_MROW_REG: the lane's operator row lives in registers for the whole kernel (28 x 16 B) instead
+// of being re-read from LDS every update
+#ifndef MH_MROW_REG
+#define MH_MROW_REG 1
+#endif
+__device__ __forceinline__ double roi_loglik(const Lds& s, const double2 (&mreg)[MLD / 2], double* e, int lane, int i,
+                                            double dvr, double r1, double k2p) {
   const double k2 = k2p * r1;           // kinetic_model.py:153-154
   const double k2a = k2 / dvr;
 #if MH_EXP_MODE & 1
@@ -171,7 +177,7 @@ __device__ __forceinline__ double roi_loglik(const Lds& s, double* e, int lane, 
     double c0 = 0.0, c1 = 0.0;
 #pragma unroll MH_MV_UNROLL
     for (int q = 0; q < MLD / 2; ++q) {
-      const double2 m = mrow[q], x = ev[q];
+      const double2 m = MH_MROW_REG ? mreg[q] : mrow[q], x = ev[q];
       c0 = fma(m.x, x.x, c0);
       c1 = fma(m.y, x.y, c1);
     }
@@ -240,6 +246,9 @@ __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun 
   __shared__ Lds s;
   load_lds(s, c);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double2 mreg[MLD / 2];
+#pragma unroll
+  for (int q = 0; q < MLD / 2; ++q) mreg[q] = reinterpret_cast<const double2*>(s.M + (lane < NF ? lane : 0) * MLD)[q];
   double* e = s.E[w];
   double* Zw = s.Z[w];
   double* LUw = s.LU[w];
@@ -269,7 +278,7 @@ __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun 
 #pragma unroll 1
     for (int i = 0; i < NR; ++i) {
       const double di = lane_bcast(D, i), ri = lane_bcast(R, i);
-      const double v = roi_loglik(s, e, lane, i, di, ri, c.k2p);
+      const double v = roi_loglik(s, mreg, e, lane, i, di, ri, c.k2p);
       if (lane == i) ll = v;
     }
     double sD = r.scaling, sR = r.scaling;
@@ -333,7 +342,7 @@ __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun 
         const double delta = Zw[k] * si;
         const double xp = xi + delta;
         const double dprior = -0.5 * (2.0 * delta * gi + delta * delta * P[i * NR + i]);
-        const double lln = roi_loglik(s, e, lane, i, v ? Di : xp, v ? xp : Ri, c.k2p);
+        const double lln = roi_loglik(s, mreg, e, lane, i, v ? Di : xp, v ? xp : Ri, c.k2p);
         const double step = dprior + lln - lli;
         const double mr = r.vs_sweep_start ? run + step : step;
         if (isfinite(mr) && LUw[k] < mr) {   // wave-uniform decision (metrop_select)
@@ -833,12 +842,15 @@ __global__ __launch_bounds__(kWaves * 64) void mh_logp_kernel(MHConst c, const d
   __shared__ Lds s;
   load_lds(s, c);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double2 mreg[MLD / 2];
+#pragma unroll
+  for (int q = 0; q < MLD / 2; ++q) mreg[q] = reinterpret_cast<const double2*>(s.M + (lane < NF ? lane : 0) * MLD)[q];
   double* e = s.E[w];
   const int li = lane < NR ? lane : 0;
   for (int pt = blockIdx.x * kWaves + w; pt < n; pt += gridDim.x * kWaves) {
     const double D = x[(size_t)pt * 2 * NR + li], R = x[(size_t)pt * 2 * NR + NR + li];
     double ll = 0.0;
-    for (int i = 0; i < NR; ++i) ll += roi_loglik(s, e, lane, i, lane_bcast(D, i), lane_bcast(R, i), c.k2p);
+    for (int i = 0; i < NR; ++i) ll += roi_loglik(s, mreg, e, lane, i, lane_bcast(D, i), lane_bcast(R, i), c.k2p);
     // MvNormal quadratic forms
     double q = 0.0;
     for (int v = 0; v < 2; ++v) {
