@@ -18,6 +18,7 @@
 // once (fold_map_kernel) and added in the epilogue together with the biases.
 // The 1x1 residual conv is folded into the centre tap of the packed weights.
 #include "petdiff_internal.h"
+#include "fp64_math.h"
 
 #include <type_traits>
 #include <algorithm>
@@ -39,6 +40,10 @@
 // The product is built with 0.
 #ifndef FIN_EXP
 #define FIN_EXP 0
+#endif
+// p_sample's Box-Muller: 1 = fdlibm-form log + sincospi (philox_normal2), 0 = ocml log + sincos
+#ifndef PETDIFF_BM_FAST
+#define PETDIFF_BM_FAST 1
 #endif
 // Tap reuse in registers (fused levels whose fragments each hold ONE position of 32 samples,
 // i.e. up0): a wave's 3 fragments sit at positions 2 (segment 1) or 1 (segment 2) apart, so the
@@ -140,9 +145,12 @@ __device__ __forceinline__ void philox_normal2(unsigned long long seed, unsigned
 #endif
   const double u1 = ((double)c[0] + 1.0) * 2.3283064365386963e-10;
   const double u2 = ((double)c[1] + 0.5) * 2.3283064365386963e-10;
-  const double r = sqrt(-2.0 * log(u1));
+  // PETDIFF_BM_FAST: fdlibm-form log (fp64_math.h, <= 1 ulp) and sincospi(2 u2) instead of ocml's log
+  // and sincos(2 pi u2); the normals agree with the oracle's to an ulp of fp64 before the f32 cast
+  const double r = sqrt(-2.0 * (PETDIFF_BM_FAST ? log_pos(u1) : log(u1)));
   double sn, cs;
-  sincos(6.283185307179586 * u2, &sn, &cs);
+  if (PETDIFF_BM_FAST) sincospi(2.0 * u2, &sn, &cs);
+  else sincos(6.283185307179586 * u2, &sn, &cs);
   z[0] = (float)(r * cs);
   z[1] = (float)(r * sn);
 }
