@@ -41,6 +41,13 @@
 #ifndef FIN_EXP
 #define FIN_EXP 0
 #endif
+// final 1x1 conv row loop (A/B switches, see the row loop)
+#ifndef FIN_SCALAR_W
+#define FIN_SCALAR_W 0
+#endif
+#ifndef FIN_SPLIT
+#define FIN_SPLIT 0
+#endif
 // p_sample's Box-Muller: 1 = fdlibm-form log + sincospi (philox_normal2), 0 = ocml log + sincos
 #ifndef PETDIFF_BM_FAST
 #define PETDIFF_BM_FAST 1
@@ -1715,8 +1722,13 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
       if constexpr ((FIN_EXP & 4) != 0) { xst[r * 2] = xst[r * 2 + 1] = fin[r * G::FIN_LD]; goto fin_rows_done; }
       const float* mp = a.tmap ? a.tmap + ((size_t)t * L + l) * cout : nullptr;
       const float* cp = a.cmap ? a.cmap + ((size_t)tac * L + l) * cout : nullptr;
-      f32x4 o4 = {0.f, 0.f, 0.f, 0.f};
-      auto dot = [&](const float* mq, const float* cq) {
+      f32x4 o4 = {0.f, 0.f, 0.f, 0.f}, o4b = {0.f, 0.f, 0.f, 0.f};
+      // FIN_SCALAR_W: with 4 outputs the final kernel [128][4] is read wave-uniformly through the
+      // scalar cache (constant address space) instead of 128 LDS reads per row.  FIN_SPLIT: odd
+      // channels accumulate separately (dependent FMA chains of 64 instead of 128).
+      typedef const __attribute__((address_space(4))) f32x4 cf32x4;
+      cf32x4* cw = (cf32x4*)(uintptr_t)f.wf;
+      auto dot = [&](const float* mq, const float* cq, auto scalar_w) {
 #pragma unroll 4
         for (int n = 0; n < 128; n += 4) {
           f32x4 hv = *reinterpret_cast<const f32x4*>(fin + r * G::FIN_LD + n);
@@ -1725,20 +1737,22 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const float hq = fmaxf(hv[q], 0.f);
-            const f32x4 wq = *reinterpret_cast<const f32x4*>(wfl + (n + q) * 4);
-            o4[0] = fmaf(hq, wq[0], o4[0]);
-            o4[1] = fmaf(hq, wq[1], o4[1]);
-            o4[2] = fmaf(hq, wq[2], o4[2]);
-            o4[3] = fmaf(hq, wq[3], o4[3]);
+            f32x4 wq;
+            if constexpr (decltype(scalar_w)::value) wq = cw[n + q];
+            else wq = *reinterpret_cast<const f32x4*>(wfl + (n + q) * 4);
+            f32x4& acc = (FIN_SPLIT && (q & 1)) ? o4b : o4;
+            acc[0] = fmaf(hq, wq[0], acc[0]);
+            acc[1] = fmaf(hq, wq[1], acc[1]);
+            acc[2] = fmaf(hq, wq[2], acc[2]);
+            acc[3] = fmaf(hq, wq[3], acc[3]);
           }
         }
       };
-      if (G::FIN_MAPS && fin_fast) {                 // the same map rows, prefetched into LDS
-        const float* lm = reinterpret_cast<const float*>(smem + G::FMAP_OFF) + l * G::FIN_LD;
-        dot(lm, lm + G::FMAP_STRIDE * 4);
-      } else {
-        dot(mp, cp);
-      }
+      const bool fin_lds = G::FIN_MAPS && fin_fast;   // the same map rows, prefetched into LDS
+      const float* lm = reinterpret_cast<const float*>(smem + G::FMAP_OFF) + l * G::FIN_LD;
+      if (FIN_SCALAR_W && n_out == 4) dot(fin_lds ? lm : mp, fin_lds ? lm + G::FMAP_STRIDE * 4 : cp, std::true_type{});
+      else dot(fin_lds ? lm : mp, fin_lds ? lm + G::FMAP_STRIDE * 4 : cp, std::false_type{});
+      if (FIN_SPLIT) o4 += o4b;
       float o[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) o[q] = o4[q] + bfin[q];
