@@ -22,3 +22,28 @@ __device__ __forceinline__ double log_pos(double x) {
   return k * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + k * 1.90821492927058770002e-10)) - f);
 }
 
+
+// e^x: x = k ln 2 + r, |r| <= ln 2 / 2 (ln 2 in two parts), e^r by its degree-13 Taylor polynomial
+// (truncation 6e-18), 2^k by ldexp: <= 1 ulp (checked against numpy).  Outside (-745, 709.7) and
+// NaN: ocml's exp (0 / inf / NaN).
+__device__ __forceinline__ double exp_fast(double x) {
+  if (!(x > -745.0 && x < 709.7)) return exp(x);
+  const double kf = rint(x * 1.4426950408889634);
+  double r = fma(-kf, 6.93147180369123816490e-01, x);
+  r = fma(-kf, 1.90821492927058770002e-10, r);
+  double p = 1.6059043836821613e-10;                       // 1/13!
+  p = fma(p, r, 2.08767569878681e-09);                     // 1/12!
+  p = fma(p, r, 2.505210838544172e-08);
+  p = fma(p, r, 2.755731922398589e-07);
+  p = fma(p, r, 2.7557319223985893e-06);
+  p = fma(p, r, 2.48015873015873e-05);
+  p = fma(p, r, 0.0001984126984126984);
+  p = fma(p, r, 0.001388888888888889);
+  p = fma(p, r, 0.008333333333333333);
+  p = fma(p, r, 0.041666666666666664);
+  p = fma(p, r, 0.16666666666666666);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  return ldexp(p, (int)kf);
+}

@@ -51,6 +51,10 @@ __device__ __forceinline__ double log_phi_poly(const double* tab, double x) {
   return p;
 }
 
+// e^{-k2a t} of the update kernel by fp64_math.h exp_fast (<= 1 ulp) instead of ocml's exp
+#ifndef MH_FAST_EXP
+#define MH_FAST_EXP 0
+#endif
 // log of the noise scale sigma > 0 (MH_FAST_LOG): fp64_math.h log_pos
 #ifndef MH_FAST_LOG
 #define MH_FAST_LOG 1
@@ -148,7 +152,8 @@ __device__ __forceinline__ double roi_loglik(const Lds& s, const double2 (&mreg)
 #if MH_EXP_MODE & 1
   e[lane] = lane < NF ? 1.0 - k2a * s.TV[lane < NF ? lane : 0] : 0.0;
 #else
-  e[lane] = lane < NF ? exp(-k2a * s.TV[lane < NF ? lane : 0]) : 0.0;   // e[54..63] = 0 (row padding)
+  const double ex = -k2a * s.TV[lane < NF ? lane : 0];
+  e[lane] = lane < NF ? (MH_FAST_EXP ? exp_fast(ex) : exp(ex)) : 0.0;   // e[54..63] = 0 (row padding)
 #endif
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
