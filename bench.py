@@ -533,15 +533,22 @@ def main():
         return model.ddpm_loop(x_T, cond, num_timesteps=n_rev, seed=2, sample_offset=offset,
                                tac=tac if n_tac > 1 else None)
 
-    for _ in range(args.warmup):
+    long_run = B > chunk                      # e.g. --config4: about a minute per step; say so on stderr
+    for i in range(args.warmup):
         out = one()
+        if long_run:
+            torch.cuda.synchronize()
+            print(f'[bench] warmup {i + 1}/{args.warmup} done', file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         out = one()
+        if long_run:                          # the sync is inside the timed region only for these runs,
+            torch.cuda.synchronize()          # where one step is ~1 minute of GPU work
+            print(f'[bench] step {i + 1}/{args.steps} done', file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
