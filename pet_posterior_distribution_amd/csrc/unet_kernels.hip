@@ -41,6 +41,10 @@
 #ifndef FIN_EXP
 #define FIN_EXP 0
 #endif
+// fused levels: issue the map prefetches after the first ring barrier (see the fused K loop)
+#ifndef CONV_MAPS_LATE
+#define CONV_MAPS_LATE 0
+#endif
 // final 1x1 conv row loop (A/B switches, see the row loop)
 #ifndef FIN_SCALAR_W
 #define FIN_SCALAR_W 0
@@ -1328,13 +1332,26 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
       __syncthreads();
     } else {
       dma.all(smem, 0, 0, lane);
-      prefetch_maps();
-      prefetch_fin_maps();
+      // CONV_MAPS_LATE: the map prefetches go out after B0 instead of right behind chunk 0.  At
+      // kernel start all 256 workgroups' bursts share the fabric, so the final level's 50 KB of map
+      // rows per workgroup would delay every chunk 0 (prologue 4.6 us on up2 against 2.8 on up0);
+      // issued after B0 they stream during the K loop and still retire at B1.
+      if constexpr (!CONV_MAPS_LATE) {
+        prefetch_maps();
+        prefetch_fin_maps();
+      }
       // B0: chunk 0 landed; the maps (issued after it, NMAPW per wave) may still be in flight --
       // B1 below retires them together with chunk 1, long before the epilogue reads them
       static_assert(NMAPW + 1 + 2 * G::PER < 64 && NMAPW + 1 + 2 * G::PER2 < 64, "vmcnt range");
-      if (map_extra) ring_barrier<NMAPW + 1>();
-      else ring_barrier<NMAPW>();
+      if constexpr (CONV_MAPS_LATE) {
+        ring_barrier<0>();
+        prefetch_maps();
+        prefetch_fin_maps();
+      } else if (map_extra) {
+        ring_barrier<NMAPW + 1>();
+      } else {
+        ring_barrier<NMAPW>();
+      }
 #if CONV_EXP_MODE & 128
       st_c0 = __builtin_amdgcn_s_memtime();
       st_r0 = __builtin_amdgcn_s_memrealtime();
