@@ -619,6 +619,57 @@ __global__ __launch_bounds__(kBW * 64) void mh_chain_batched(MHConst c, MHRun r)
     // numbers, scans and keeps the statistics; it hands D, R and the proposals to the others
     // through LDS once per draw (a redundant scan in every wave would triple its issue cost)
     const bool lead = WPC == 1 || rk == 0;
+    // the sweep's random numbers of draw `itn` (N(0,1) proposals, log accept uniforms, shuffled
+    // order) into the scratch of the wave that runs it
+    auto draw_rng = [&](int itn, double* Zx, double* LUx, uint32_t* KEYx, int* ORDx) {
+      if (MH_BEXP & 16) {                  // diagnostic: identity order, no RNG
+        for (int h = 0; h < 2; ++h) {
+          const int k = lane + 64 * h;
+          if (k < 2 * NR) { Zx[k] = 0.5; LUx[k] = -1.0; ORDx[k] = k; }
+        }
+        return;
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = lane + 64 * h;
+        if (k < 2 * NR) {
+          uint32_t q[4] = {(uint32_t)k, (uint32_t)itn, ch_lo, ch_hi};
+          philox(q, sk0, sk1);
+          const double u1 = ((double)q[0] + 1.0) * 2.3283064365386963e-10;
+          const double u2 = ((double)q[1] + 0.5) * 2.3283064365386963e-10;
+          Zx[k] = sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
+          LUx[k] = log(((double)q[2] + 0.5) * 2.3283064365386963e-10);
+          KEYx[k] = q[3];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = lane + 64 * h;
+        if (k < 2 * NR) {
+          const uint32_t kk = KEYx[k];
+          int rank = 0;
+#pragma unroll 8
+          for (int j = 0; j < 2 * NR; ++j) {
+            const uint32_t kj = KEYx[j];
+            rank += (kj < kk) | ((kj == kk) & (j < k));
+          }
+          ORDx[rank] = k;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    };
+    // waves_per_chain > 1: the group's second wave draws the NEXT draw's random numbers while the
+    // leader scans (they do not depend on the sweep), into its own scratch; the leader reads them
+    // after the end-of-draw barrier
+    double* Wh = s.W[grp * WPC + (WPC > 1 ? 1 : 0)];
+    if constexpr (WPC > 1) {               // the first draw's numbers come from the helper too
+      if (rk == 1 && total > 0)
+        draw_rng(0, Wh, Wh + 2 * NR, reinterpret_cast<uint32_t*>(Wh + 4 * NR), reinterpret_cast<int*>(Wh + 5 * NR));
+      __syncthreads();
+    }
     for (int it = 0; it < total; ++it) {
       double dD = 0.0, dR = 0.0, luD = 0.0, luR = 0.0;
       int ordA = 0, ordB = 0;
@@ -628,51 +679,20 @@ __global__ __launch_bounds__(kBW * 64) void mh_chain_batched(MHConst c, MHRun r)
           sR = tune_scale(sR, (double)aR / r.tune_interval);
           aD = aR = 0;
         }
-        if (MH_BEXP & 16) {                // diagnostic: identity order, no RNG
-          for (int h = 0; h < 2; ++h) {
-            const int k = lane + 64 * h;
-            if (k < 2 * NR) { Zw[k] = 0.5; LUw[k] = -1.0; ORDw[k] = k; }
-          }
-        } else
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int k = lane + 64 * h;
-          if (k < 2 * NR) {
-            uint32_t q[4] = {(uint32_t)k, (uint32_t)it, ch_lo, ch_hi};
-            philox(q, sk0, sk1);
-            const double u1 = ((double)q[0] + 1.0) * 2.3283064365386963e-10;
-            const double u2 = ((double)q[1] + 0.5) * 2.3283064365386963e-10;
-            Zw[k] = sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
-            LUw[k] = log(((double)q[2] + 0.5) * 2.3283064365386963e-10);
-            KEYw[k] = q[3];
-          }
+        double* Zs = Wh;                   // waves_per_chain > 1: the helper's draw
+        if constexpr (WPC == 1) {
+          draw_rng(it, Zw, LUw, KEYw, ORDw);
+          Zs = Zw;
         }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        if (!(MH_BEXP & 16))
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int k = lane + 64 * h;
-          if (k < 2 * NR) {
-            const uint32_t kk = KEYw[k];
-            int rank = 0;
-#pragma unroll 8
-            for (int j = 0; j < 2 * NR; ++j) {
-              const uint32_t kj = KEYw[j];
-              rank += (kj < kk) | ((kj == kk) & (j < k));
-            }
-            ORDw[rank] = k;
-          }
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        const double* LUs = Zs + 2 * NR;
+        const int* ORDs = reinterpret_cast<const int*>(Zs + 5 * NR);
         // to registers: lane i holds its ROI's two proposals / accept uniforms, lane j the order
-        dD = Zw[li] * sD;
-        dR = Zw[NR + li] * sR;
-        luD = LUw[li];
-        luR = LUw[NR + li];
-        ordA = ORDw[lane];
-        ordB = ORDw[64 + (lane & 31)];
+        dD = Zs[li] * sD;
+        dR = Zs[NR + li] * sR;
+        luD = LUs[li];
+        luR = LUs[NR + li];
+        ordA = ORDs[lane];
+        ordB = ORDs[64 + (lane & 31)];
         __builtin_amdgcn_wave_barrier();
       }
       double pD = D + dD, pR = R + dR;
@@ -707,6 +727,10 @@ __global__ __launch_bounds__(kBW * 64) void mh_chain_batched(MHConst c, MHRun r)
       }
       if constexpr (WPC > 1) __syncthreads();
       else { __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); }
+      if (WPC > 1 && rk == 1 && it + 1 < total) {
+        uint32_t* KEYh = reinterpret_cast<uint32_t*>(Wh + 4 * NR);
+        draw_rng(it + 1, Wh, Wh + 2 * NR, KEYh, reinterpret_cast<int*>(Wh + 5 * NR));
+      }
       // (the leader reads LLg below; the others next write it after the next draw's hand-off
       // barrier, which the leader joins only after its scan)
       // ---- the sweep: wave-uniform scan over the shuffled order.  An accept adds delta times
@@ -804,6 +828,7 @@ __global__ __launch_bounds__(kBW * 64) void mh_chain_batched(MHConst c, MHRun r)
         mR += dr / (double)nk;
         m2R = fma(dr, R - mR, m2R);
       }
+      if constexpr (WPC > 1) __syncthreads();   // the helper's next draw is in its scratch
     }
     if (own && store) {
       double* st = r.stats + (size_t)chain * 2 * NR * 3;
