@@ -134,71 +134,37 @@ def host_threads():
 
 
 def cpu_baseline(weights, cond, budget_s=15.0):
-    """Oracle (NumPy fp32 restatement) on a bounded sample: B=32 samples, as many reverse
-    steps as fit in ~budget_s, extrapolated to the 1000-step process.  BLAS threads are
-    limited to the job's CPU share (host_threads)."""
+    """The oracle's p_sample on the host CPU, bounded: oracle/iddpm_torch_cpu.py (the NumPy oracle
+    restated with torch's CPU conv1d, 2.4x its rate; checked against it in tests/test_cpu.py),
+    fp32, B = 256 samples of configs[1]'s TAC, as many reverse steps as fit in ~budget_s, extrapolated
+    to the 1000-step process.  Threads: the job's CPU share (host_threads)."""
+    import torch
     from oracle import iddpm_ref as R
+    from oracle import iddpm_torch_cpu as TC
     cores = host_threads()
-    try:
-        from threadpoolctl import threadpool_limits
-        limiter = threadpool_limits(cores)
-    except Exception:
-        limiter = None
+    prev = torch.get_num_threads()
+    torch.set_num_threads(cores)
     S = R.schedule_tables(R.get_beta_schedule('cosine', 1000))
     rng = np.random.default_rng(0)
-    B = 32
-    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
-    c = np.repeat(cond[None], B, 0)
-    P = {k: v.astype(np.float32) for k, v in weights.items()}
+    B = 256
+    x = torch.as_tensor(rng.standard_normal((B, 48, 2)).astype(np.float32))
+    c = torch.as_tensor(np.repeat(np.asarray(cond, np.float32)[None], B, 0))
+    net = TC.TorchCpuUnet({k: v.astype(np.float32) for k, v in weights.items()})
+    net.ddpm(S, x, np.full(B, 999, np.int32), c, torch.zeros_like(x))      # warm-up (oneDNN primitives)
     n, t0 = 0, time.perf_counter()
     for ti in R.loop_indices(1000):
-        z = rng.standard_normal((B, 48, 2)).astype(np.float32)
-        m, _, vt = R.ddpm(P, S, x, np.full(B, ti, np.int32), c, z, dt=np.float32)
+        z = torch.as_tensor(rng.standard_normal((B, 48, 2)).astype(np.float32))
+        m, _, vt = net.ddpm(S, x, np.full(B, ti, np.int32), c, z)
         x = m + vt
         n += 1
         if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
-    if limiter is not None:
-        limiter.unregister()
+    torch.set_num_threads(prev)
     per_step = dt / n
     return {'value': B / (per_step * 1000.0), 'unit': 'samples/s', 'cores': int(cores), 'kind': 'port',
-            'sample': f'oracle/iddpm_ref.py NumPy fp32, B=32 samples x {n} reverse steps ({dt:.1f} s), '
-                      f'extrapolated to 1000 steps'}
-
-
-def load_pmc(fused_up=False):
-    """Per-launch PMC figures of the dominant kernel from the committed rocprofv3 summary
-    (profiles/pmc_traffic.json): HBM bytes (FETCH_SIZE x2 + WRITE_SIZE), SQ_VALU_MFMA_BUSY_CYCLES
-    and GRBM_GUI_ACTIVE; missing entries are None."""
-    pre = 'up0_fused' if fused_up else 'up0_block'
-    p = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
-    try:
-        with open(p) as f:
-            d = json.load(f)
-    except Exception:
-        d = {}
-    return {k: d.get(pre + suf) for k, suf in (('traffic', '_bytes_per_launch'), ('mfma_busy', '_mfma_busy_cycles'),
-                                                ('grbm', '_grbm_gui_active'), ('source', '_source'))}
-
-
-def pmc_fields(pmc, avg_s):
-    """HBM GB/s and MFMA utilisation of the dominant kernel against chip peak.
-    SQ_VALU_MFMA_BUSY_CYCLES = 32 cycles per 32x32x16 MFMA (MI355X_MICROARCH.md), summed over the
-    1024 SIMDs.  mfma_util = busy / (1024 x 2.4 GHz x launch time): the MFMA pipes' share of the
-    peak-clock cycles (the same ratio as executed FLOP/s / dense peak).  mfma_busy_vs_active divides
-    by the kernel's own active cycles instead (GRBM_GUI_ACTIVE / 8 XCDs), which the guide notes
-    reads high on dispatches this short, so that fraction reads low."""
-    out = {'hbm_gbs': None, 'hbm_frac': None, 'mfma_util': None, 'mfma_busy_vs_active': None}
-    if pmc['traffic']:
-        out['hbm_gbs'] = round(pmc['traffic'] / avg_s / 1e9, 1)
-        out['hbm_frac'] = round(pmc['traffic'] / avg_s / 1e9 / PEAK_HBM_GBS, 4)
-    if pmc['mfma_busy']:
-        out['mfma_util'] = round(pmc['mfma_busy'] / (N_SIMD * PEAK_CLOCK_HZ * avg_s), 4)
-        if pmc['grbm']:
-            out['mfma_busy_vs_active'] = round(pmc['mfma_busy'] / (N_SIMD * pmc['grbm'] / 8), 4)
-    out['pmc_source'] = pmc['source']
-    return out
+            'sample': f'oracle/iddpm_torch_cpu.py (the oracle on torch CPU conv1d) fp32, B={B} samples x {n} '
+                      f'reverse steps ({dt:.1f} s), extrapolated to 1000 steps'}
 
 
 # MH cost per element update (one ROI's SRTM2 + 54 truncated-normal terms), counted

@@ -355,3 +355,26 @@ def test_default_noise_stream_keys_distinct():
     assert len(keys) == 4 * 3 * 50
     assert all(0 <= k < 2 ** 64 for k in keys)
     assert stream_seed(12345, STREAM_LOOP, 0) not in (12345, 12346)
+
+
+def test_torch_cpu_baseline_port_matches_oracle():
+    """oracle/iddpm_torch_cpu.py (the CPU-baseline timing port) computes the NumPy oracle's
+    p_sample: fp32 both, same weights, t, condition and z."""
+    import torch
+    from oracle import iddpm_torch_cpu as TC
+    from pet_posterior_distribution_amd import networks as N
+    w = N.glorot_uniform_init(R.param_spec(), seed=3, bias_scale=0.05)
+    P = {k: np.asarray(v, np.float32) for k, v in w.items()}
+    S = R.schedule_tables(R.get_beta_schedule('cosine', 1000))
+    rng = np.random.default_rng(4)
+    B = 3
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    t = np.array([0, 500, 999], np.int32)
+    cond = rng.standard_normal((B, 49, 54)).astype(np.float32)
+    z = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    m_ref, v_ref, vt_ref = R.ddpm(P, S, x, t, cond, z, dt=np.float32)
+    net = TC.TorchCpuUnet(P)
+    m, v, vt = net.ddpm(S, torch.as_tensor(x), t, torch.as_tensor(cond), torch.as_tensor(z))
+    for a, b in ((m, m_ref), (vt, vt_ref)):
+        a = a.numpy()
+        assert np.abs(a - b).max() <= 2e-5 * max(1.0, np.abs(b).max()), np.abs(a - b).max()
