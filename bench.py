@@ -167,6 +167,40 @@ def cpu_baseline(weights, cond, budget_s=15.0):
                       f'reverse steps ({dt:.1f} s), extrapolated to 1000 steps'}
 
 
+def load_pmc(fused_up=False):
+    """Per-launch PMC figures of the dominant kernel from the committed rocprofv3 summary
+    (profiles/pmc_traffic.json): HBM bytes (FETCH_SIZE x2 + WRITE_SIZE), SQ_VALU_MFMA_BUSY_CYCLES
+    and GRBM_GUI_ACTIVE; missing entries are None."""
+    pre = 'up0_fused' if fused_up else 'up0_block'
+    p = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+    try:
+        with open(p) as f:
+            d = json.load(f)
+    except Exception:
+        d = {}
+    return {k: d.get(pre + suf) for k, suf in (('traffic', '_bytes_per_launch'), ('mfma_busy', '_mfma_busy_cycles'),
+                                                ('grbm', '_grbm_gui_active'), ('source', '_source'))}
+
+
+def pmc_fields(pmc, avg_s):
+    """HBM GB/s and MFMA utilisation of the dominant kernel against chip peak.
+    SQ_VALU_MFMA_BUSY_CYCLES = 32 cycles per 32x32x16 MFMA (MI355X_MICROARCH.md), summed over the
+    1024 SIMDs.  mfma_util = busy / (1024 x 2.4 GHz x launch time): the MFMA pipes' share of the
+    peak-clock cycles (the same ratio as executed FLOP/s / dense peak).  mfma_busy_vs_active divides
+    by the kernel's own active cycles instead (GRBM_GUI_ACTIVE / 8 XCDs), which the guide notes
+    reads high on dispatches this short, so that fraction reads low."""
+    out = {'hbm_gbs': None, 'hbm_frac': None, 'mfma_util': None, 'mfma_busy_vs_active': None}
+    if pmc['traffic']:
+        out['hbm_gbs'] = round(pmc['traffic'] / avg_s / 1e9, 1)
+        out['hbm_frac'] = round(pmc['traffic'] / avg_s / 1e9 / PEAK_HBM_GBS, 4)
+    if pmc['mfma_busy']:
+        out['mfma_util'] = round(pmc['mfma_busy'] / (N_SIMD * PEAK_CLOCK_HZ * avg_s), 4)
+        if pmc['grbm']:
+            out['mfma_busy_vs_active'] = round(pmc['mfma_busy'] / (N_SIMD * pmc['grbm'] / 8), 4)
+    out['pmc_source'] = pmc['source']
+    return out
+
+
 # MH cost per element update (one ROI's SRTM2 + 54 truncated-normal terms), counted
 # from mh_kernels.hip: 54x54 operator FMAs + per-frame exp/sqrt/div/log/erfc/log.
 MH_FP64_FLOP_PER_UPDATE = 2 * 54 * 54 + 54 * 120
