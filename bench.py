@@ -48,6 +48,14 @@ EXEC_FLOP_PER_SAMPLE_STEP_UNFUSED = 2 * (48 * 6 * 2 * 128 + 24 * 6 * 128 * 256 +
                                          6 * 6 * 512 * 1024 + 12 * 2 * 1024 * 512 + 12 * 6 * 1024 * 512 +
                                          24 * 2 * 512 * 256 + 24 * 6 * 512 * 256 + 48 * 2 * 256 * 128 +
                                          48 * 6 * 256 * 128 + 48 * 128 * 4)
+# MFMA FLOP the 16-bit path executes per sample-step: down1, down2 / down3 with their zero taps skipped
+# (position-major: 63 / 72 and 54 / 72 of the (fragment, tap) products), and the fused up levels
+# (skip half 6 taps + 2-phase composite 4 taps + the two left-edge correction rows); down0 and the
+# final 1x1 conv run on VALU and are not counted
+EXEC_MFMA_FLOP_PER_SAMPLE_STEP_FUSED = int(
+    2 * 24 * 6 * 128 * 256 + 2 * 12 * 6 * 256 * 512 * 63 / 72 + 2 * 6 * 6 * 512 * 1024 * 54 / 72 +
+    sum(2 * L * 6 * cs * co + 2 * L * 4 * cb * co + 2 * 2 * cb * co
+        for L, cs, cb, co in ((12, 512, 1024, 512), (24, 256, 512, 256), (48, 128, 256, 128))))
 # training step: forward + data grad + weight grad of every layer, incl. the
 # per-sample condition encoder / label projections / time MLP (6,002,304 FLOP per sample forward)
 TRAIN_FLOP_PER_SAMPLE = 3 * (FLOP_PER_SAMPLE_STEP + 6_002_304)
@@ -413,6 +421,34 @@ def f32_exact_rate(cond, B, n_rev, dev):
                     'the centre tap, so they execute 0.82 of that (executed_frac) and frac can exceed 1'}
 
 
+def bf16x3_rate(cond, B, n_rev, dev):
+    """fp32-class accuracy on the bf16 MFMA path (PETDIFF_DTYPE_BF16X3: every fp32 operand split
+    hi + lo into bf16, three products per pair, fp32 accumulate; tests/test_gpu_bf16x3.py holds it to
+    the exact-f32 mode's 1e-4 parity bounds).  Same generate() as f32_exact_rate; frac counts the
+    algorithmic FLOPs against the dense bf16 peak, executed_frac the 3 x executed bf16 MFMA FLOPs."""
+    import torch
+    from pet_posterior_distribution_amd import ImprovedDDPM, UnetConditional
+    from pet_posterior_distribution_amd.configs import shipped_net_args, shipped_diff_args
+    net = UnetConditional(**shipped_net_args(), seed=1234)
+    net.build((None, 48, 2))
+    m = ImprovedDDPM(network=net, dtype='bf16x3', device=dev.index, **shipped_diff_args())
+    x = m.philox_normal(B, seed=5)
+    m.ddpm_loop(x, cond[None], num_timesteps=n_rev, seed=2)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = m.ddpm_loop(x, cond[None], num_timesteps=n_rev, seed=2)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    tf = FLOP_PER_SAMPLE_STEP * n_rev * B / el / 1e12
+    te = 3 * EXEC_MFMA_FLOP_PER_SAMPLE_STEP_FUSED * n_rev * B / el / 1e12
+    m.close()
+    return {'value': round(B / el, 2), 'unit': 'samples/s', 'dtype': 'bf16x3 (fp32-class)', 'n_posterior': B,
+            'reverse_steps': n_rev, 'ms_per_generate': round(el * 1e3, 2),
+            'pipeline_tflops': round(tf, 2), 'frac_vs_f32_peak': round(tf / PEAK_F32_TFLOPS, 4),
+            'executed_bf16_tflops': round(te, 2), 'executed_frac': round(te / PEAK_BF16_TFLOPS, 4),
+            'finite': bool(torch.isfinite(out).all())}
+
+
 def mh_slice_and_protocol(iddpm_10k_s, dev):
     """BASELINE configs[2] slice (10k chains x 500 steps of the 20k) and the reference's per-TAC
     MCMC protocol (main_script.py:363-364, pymc's default 4 chains: 4 x (20k draws + 40k tune)),
@@ -630,6 +666,7 @@ def main():
             line['cpu_baseline'] = None
         if world == 1 and not args.no_extras and args.dtype == 'bfloat16' and n_rev == 1000 and n_tac == 1:
             line['f32_exact'] = f32_exact_rate(cond[0], B, n_rev, dev)
+            line['bf16x3'] = bf16x3_rate(cond[0], B, n_rev, dev)
             t10k = iddpm_10k_seconds(model, cond[0])
             line['mh_config3_slice'], line['reference_protocol'] = mh_slice_and_protocol(t10k, dev)
             line['weights_sensitivity'] = weights_sensitivity(net, cond[0], B, dev)

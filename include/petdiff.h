@@ -66,6 +66,10 @@ extern "C" {
 #define PETDIFF_DTYPE_F32 0        /* exact-f32 MFMA network (parity mode)    */
 #define PETDIFF_DTYPE_BF16 1       /* bf16 MFMA network, fp32 accumulate + fp32 p_sample */
 #define PETDIFF_DTYPE_F16 2        /* fp16 MFMA network (BASELINE config 5), fp32 accumulate + p_sample */
+#define PETDIFF_DTYPE_BF16X3 3     /* fp32-class network on the bf16 MFMA path: every fp32 operand split
+                                      hi + lo into bf16, products hi*hi + hi*lo + lo*hi (3 MFMAs), fp32
+                                      accumulate; about 2^-16 relative per product, meets the 1e-4 parity
+                                      tolerance of the exact-f32 mode */
 
 #define PETDIFF_LEARN_FIXED 0      /* learn_variance = ''            */
 #define PETDIFF_LEARN 1            /* 'learn'                         */

@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('PETDIFF_LIB') or os.path.join(_HERE, 'libpetdiff.so')
 
 PETDIFF_OK, PETDIFF_ERR_INVALID, PETDIFF_ERR_HIP, PETDIFF_ERR_UNSUPPORTED = 0, 1, 2, 3
-DTYPE_F32, DTYPE_BF16, DTYPE_F16 = 0, 1, 2
+DTYPE_F32, DTYPE_BF16, DTYPE_F16, DTYPE_BF16X3 = 0, 1, 2, 3
 LEARN_FIXED, LEARN, LEARN_RANGED = 0, 1, 2
 PARAM_EPS, PARAM_X0, PARAM_V, PARAM_XPREV = 0, 1, 2, 3
 NTAB = 13

@@ -165,13 +165,32 @@ struct petdiff_ctx {
   size_t ev_next = 0;
 
   const float* W(const std::string& n) const { return w32.as<float>() + off.at(n); }
-  size_t act_bytes() const { return cfg.dtype == PETDIFF_DTYPE_F32 ? 4 : 2; }
+  // bf16x3 (PETDIFF_DTYPE_BF16X3): activations are [hi | lo] bf16 rows, 4 bytes per value
+  bool x3 = false;
+  size_t act_bytes() const { return (cfg.dtype == PETDIFF_DTYPE_F32 || x3) ? 4 : 2; }
 };
 
 namespace {
 
 // XOR key of the 16-B piece index within a packed weight row n (= ConvGeom::key)
 int piece_key(int n, int cpr) { return cpr == 4 ? ((n >> 2) & 3) : cpr == 2 ? ((n >> 3) & 1) : ((n >> 1) & 7); }
+
+// K chunks of a packed weight tile in kernel order: (channel chunk, part) with part 0 = the value
+// (bf16x3: its hi half) and 1 = its lo half.  bf16x3 walks every input segment of nc chunks three
+// times -- (a_hi, w_hi), (a_hi, w_lo), (a_lo, w_hi) -- see DmaPlan in unet_kernels.hip.
+std::vector<std::pair<int, int>> chunk_order(int nc1, int nc2, bool x3) {
+  std::vector<std::pair<int, int>> o;
+  for (int seg = 0; seg < 2; ++seg) {
+    const int base = seg ? nc1 : 0, n = seg ? nc2 : nc1;
+    for (int g = 0; g < (x3 ? 3 : 1); ++g)
+      for (int k = 0; k < n; ++k) o.push_back({base + k, g == 1 ? 1 : 0});
+  }
+  return o;
+}
+
+float bf_hi(float v) { const uint32_t u = (uint32_t)f2bf(v) << 16; float f; std::memcpy(&f, &u, 4); return f; }
+// part 1 of a bf16x3 weight: the bf16 of its residual after the hi half
+float split_part(float v, int part) { return part ? v - bf_hi(v) : v; }
 
 template <typename T, typename H>
 int pack_conv(petdiff_ctx* h, const std::vector<float>& wk_host, int li) {
@@ -193,21 +212,25 @@ int pack_conv(petdiff_ctx* h, const std::vector<float>& wk_host, int li) {
   if (cl.cin_x % KC != 0) return fail(PETDIFF_ERR_UNSUPPORTED, "channel count not a multiple of the K chunk");
   if (cl.cout % NT != 0) return fail(PETDIFF_ERR_UNSUPPORTED, "cout not a multiple of the N tile");
   const int NC = cl.cin_x / KC, nNT = cl.cout / NT;
+  // the up blocks read [skip | u] from two inputs of cin_x / 2 channels each (run_network's lio)
+  const bool two = cl.xoff == 0 && cl.cond_level < 0;
+  const auto order = chunk_order(two ? NC / 2 : NC, two ? NC / 2 : 0, h->x3);
   // [n_tile][chunk][tap][n (NT)][CPR x 16-B pieces], piece index XOR-swizzled by n
   // exactly like ConvGeom::key so a linear LDS-DMA copy yields the swizzled image.
-  std::vector<H> out((size_t)nNT * NC * cl.taps * NT * KC);
+  std::vector<H> out((size_t)nNT * order.size() * cl.taps * NT * KC);
   size_t q = 0;
   for (int nt = 0; nt < nNT; ++nt)
-    for (int kc = 0; kc < NC; ++kc)
+    for (const auto& ck : order)
       for (int j = 0; j < cl.taps; ++j)
         for (int n = 0; n < NT; ++n)
           for (int p = 0; p < CPR; ++p) {
             const int c = p ^ piece_key(n, CPR);
             for (int e = 0; e < EPC; ++e) {
-              const int ci = cl.xoff + kc * KC + c * EPC + e;
+              const int ci = cl.xoff + ck.first * KC + c * EPC + e;
               const int co = nt * NT + n;
               float v = wk[((size_t)j * cl.cin_full + ci) * cl.cout + co];
               if (wr && j == cl.padl) v += wr[(size_t)ci * cl.cout + co];
+              v = split_part(v, ck.second);
               if constexpr (std::is_same<T, f16>::value) out[q++] = f2h(v);
               else if constexpr (sizeof(H) == 2) out[q++] = f2bf(v);
               else out[q++] = v;
@@ -257,36 +280,40 @@ int pack_fused(petdiff_ctx* h, const std::vector<float>& host, int u) {
     if constexpr (std::is_same<T, f16>::value) return f2h(v);
     else return f2bf(v);
   };
-  std::vector<H> out((size_t)nNT * (n1 * 6 + n2 * 8) * NT * KC);
-  std::vector<H> eout((size_t)nNT * n2 * 2 * NT * KC);
+  const int x3 = h->x3 ? 3 : 1;
+  const auto order1 = chunk_order(n1, 0, h->x3), order2 = chunk_order(n2, 0, h->x3);
+  std::vector<H> out((size_t)nNT * x3 * (n1 * 6 + n2 * 8) * NT * KC);
+  std::vector<H> eout((size_t)nNT * x3 * n2 * 2 * NT * KC);
   size_t q = 0, qe = 0;
   for (int nt = 0; nt < nNT; ++nt) {
-    for (int kc = 0; kc < n1; ++kc)
+    for (const auto& ck : order1)
       for (int j = 0; j < 6; ++j)
         for (int n = 0; n < NT; ++n)
           for (int p = 0; p < CPR; ++p) {
             const int c = p ^ piece_key(n, CPR);
             for (int e = 0; e < EPC; ++e) {
-              const int ci = kc * KC + c * EPC + e, co = nt * NT + n;
+              const int ci = ck.first * KC + c * EPC + e, co = nt * NT + n;
               float v = wk[((size_t)j * blk.cin_full + ci) * blk.cout + co];
               if (j == blk.padl) v += wr[(size_t)ci * blk.cout + co];
-              out[q++] = cvt(v);
+              out[q++] = cvt(split_part(v, ck.second));
             }
           }
-    for (int kc = 0; kc < n2; ++kc) {
+    for (const auto& ck : order2) {
+      const int kc = ck.first;
       for (int t = 0; t < 8; ++t)
         for (int n = 0; n < NT; ++n)
           for (int p = 0; p < CPR; ++p) {
             const int c = p ^ piece_key(n, CPR);
             for (int e = 0; e < EPC; ++e) {
               const int cb = kc * KC + c * EPC + e, co = nt * NT + n;
-              out[q++] = cvt(D[((size_t)t * fl.cb + cb) * fl.cout + co]);
+              out[q++] = cvt(split_part(D[((size_t)t * fl.cb + cb) * fl.cout + co], ck.second));
             }
           }
       for (int ph = 0; ph < 2; ++ph)
         for (int n = 0; n < NT; ++n)
           for (int kk = 0; kk < KC; ++kk)
-            eout[qe++] = cvt(D[((size_t)(8 + ph) * fl.cb + kc * KC + kk) * fl.cout + nt * NT + n]);
+            eout[qe++] = cvt(split_part(D[((size_t)(8 + ph) * fl.cb + kc * KC + kk) * fl.cout + nt * NT + n],
+                                        ck.second));
     }
   }
   HIPC(h->wpack_f[u].alloc(out.size() * sizeof(H)));
@@ -413,7 +440,7 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
   d0.s0 = s0;
   d0.p0 = p0;
   d0.B = B;
-  if (!io.skip_down0) CHK(timed(0, [&] { return launch_down0<T>(d0, s); }));
+  if (!io.skip_down0) CHK(timed(0, [&] { return launch_down0<T>(d0, s, h->x3); }));
 
   struct LIO { const void* s1; int c1; const void* s2; int c2; void* out; void* pool; };
   const LIO lio[kNumConvLayers] = {
@@ -464,7 +491,7 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
           a.fin.next.s0 = s0_other;
         }
       }
-      CHK(timed(1 + li, [&] { return launch_conv<T>(fl.kind, a, s); }));
+      CHK(timed(1 + li, [&] { return launch_conv<T>(fl.kind, a, s, h->x3); }));
       continue;
     }
     ConvArgs<T> a{};
@@ -502,7 +529,7 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
         a.fin.next.s0 = s0_other;
       }
     }
-    CHK(timed(1 + li, [&] { return launch_conv<T>(cl.kind, a, s); }));
+    CHK(timed(1 + li, [&] { return launch_conv<T>(cl.kind, a, s, h->x3); }));
   }
   return PETDIFF_OK;
 }
@@ -510,7 +537,7 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
 int network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
   if (!h->sched_set) return fail(PETDIFF_ERR_INVALID, "schedule not set (petdiff_set_schedule)");
   if (h->n_tac <= 0) return fail(PETDIFF_ERR_INVALID, "conditions not set (petdiff_set_conditions)");
-  if (h->cfg.dtype == PETDIFF_DTYPE_BF16) return run_network<bf16>(h, io, B, s);
+  if (h->cfg.dtype == PETDIFF_DTYPE_BF16 || h->x3) return run_network<bf16>(h, io, B, s);
   if (h->cfg.dtype == PETDIFF_DTYPE_F16) return run_network<f16>(h, io, B, s);
   return run_network<float>(h, io, B, s);
 }
@@ -589,8 +616,10 @@ int petdiff_create(const petdiff_config* cfg, const float* weights, size_t n_wei
   if (!is_shipped_arch(*cfg))
     return fail(PETDIFF_ERR_UNSUPPORTED,
                 "only the shipped UnetConditional (f128/d4, k6, L48, enc 256-128-64-32) is compiled");
-  if (cfg->dtype != PETDIFF_DTYPE_F32 && cfg->dtype != PETDIFF_DTYPE_BF16 && cfg->dtype != PETDIFF_DTYPE_F16)
-    return fail(PETDIFF_ERR_INVALID, "dtype must be PETDIFF_DTYPE_F32, PETDIFF_DTYPE_BF16 or PETDIFF_DTYPE_F16");
+  if (cfg->dtype != PETDIFF_DTYPE_F32 && cfg->dtype != PETDIFF_DTYPE_BF16 && cfg->dtype != PETDIFF_DTYPE_F16 &&
+      cfg->dtype != PETDIFF_DTYPE_BF16X3)
+    return fail(PETDIFF_ERR_INVALID,
+                "dtype must be PETDIFF_DTYPE_F32, PETDIFF_DTYPE_BF16, PETDIFF_DTYPE_F16 or PETDIFF_DTYPE_BF16X3");
   if (cfg->learn_variance < 0 || cfg->learn_variance > 2 || cfg->parameterization < 0 ||
       cfg->parameterization > 3)
     return fail(PETDIFF_ERR_INVALID, "bad learn_variance / parameterization");
@@ -598,6 +627,7 @@ int petdiff_create(const petdiff_config* cfg, const float* weights, size_t n_wei
   h->cfg = *cfg;
   h->device = device;
   h->n_out = cfg->learn_variance == PETDIFF_LEARN_FIXED ? cfg->n_par : 2 * cfg->n_par;
+  h->x3 = cfg->dtype == PETDIFF_DTYPE_BF16X3;
   h->spec = make_spec(*cfg, h->n_out);
   if (const char* e = std::getenv("PETDIFF_FUSE_DOWN0")) h->fuse_down0 = std::atoi(e) != 0;
   h->fuse_up = cfg->dtype != PETDIFF_DTYPE_F32;
@@ -619,7 +649,7 @@ int petdiff_create(const petdiff_config* cfg, const float* weights, size_t n_wei
   HIPC(hipMemcpy(h->w32.p, weights, need * 4, hipMemcpyHostToDevice));
   std::vector<float> host(weights, weights + need);
   for (int li = 0; li < kNumConvLayers; ++li) {
-    if (cfg->dtype == PETDIFF_DTYPE_BF16) CHK((pack_conv<bf16, uint16_t>(h.get(), host, li)));
+    if (cfg->dtype == PETDIFF_DTYPE_BF16 || h->x3) CHK((pack_conv<bf16, uint16_t>(h.get(), host, li)));
     else if (cfg->dtype == PETDIFF_DTYPE_F16) CHK((pack_conv<f16, uint16_t>(h.get(), host, li)));
     else CHK((pack_conv<float, float>(h.get(), host, li)));
     const ConvLayer& cl = kConv[li];
@@ -634,7 +664,7 @@ int petdiff_create(const petdiff_config* cfg, const float* weights, size_t n_wei
   }
   if (h->fuse_up)
     for (int u = 0; u < 3; ++u) {
-      if (cfg->dtype == PETDIFF_DTYPE_BF16) CHK((pack_fused<bf16, uint16_t>(h.get(), host, u)));
+      if (cfg->dtype == PETDIFF_DTYPE_BF16 || h->x3) CHK((pack_fused<bf16, uint16_t>(h.get(), host, u)));
       else CHK((pack_fused<f16, uint16_t>(h.get(), host, u)));
     }
   // down0: x channels 50, 51 of down0.conv (6, 52, 128) with the res kernel folded into tap 2
@@ -913,7 +943,9 @@ int petdiff_get_activation(petdiff_handle h, int level, float* out, int B, void*
   const size_t n = (size_t)B * per[level];
   hipStream_t s = (hipStream_t)stream;
   const void* src = bufs[level]->p;
-  if (h->cfg.dtype == PETDIFF_DTYPE_BF16) HIPC(launch_to_f32<bf16>(static_cast<const bf16*>(src), n, out, s));
+  static const int chan[PETDIFF_NUM_LEVELS] = {128, 256, 512, 1024, 512, 256};
+  if (h->x3) HIPC(launch_split_to_f32(static_cast<const bf16*>(src), n / chan[level], chan[level], out, s));
+  else if (h->cfg.dtype == PETDIFF_DTYPE_BF16) HIPC(launch_to_f32<bf16>(static_cast<const bf16*>(src), n, out, s));
   else if (h->cfg.dtype == PETDIFF_DTYPE_F16) HIPC(launch_to_f32<f16>(static_cast<const f16*>(src), n, out, s));
   else HIPC(launch_to_f32<float>(static_cast<const float*>(src), n, out, s));
   return PETDIFF_OK;

@@ -86,10 +86,12 @@ struct ConvArgs {
 
 
 // Launch helpers (unet_kernels.hip).  Return hipError_t.
+// x3: the bf16x3 network (T = bf16 only; activations stored as [hi | lo] rows, see DmaPlan)
 template <typename T>
-hipError_t launch_conv(int layer_kind, const ConvArgs<T>& a, hipStream_t s);
+hipError_t launch_conv(int layer_kind, const ConvArgs<T>& a, hipStream_t s, bool x3 = false);
 template <typename T>
-hipError_t launch_down0(const Down0Args& a, hipStream_t s);
+hipError_t launch_down0(const Down0Args& a, hipStream_t s, bool x3 = false);
+hipError_t launch_split_to_f32(const bf16* src, size_t rows, int C, float* dst, hipStream_t s);
 
 hipError_t launch_set_rng(unsigned long long* dst, unsigned long long seed, unsigned long long off0,
                           unsigned long long off1, int parts, hipStream_t s);

@@ -438,22 +438,34 @@ __device__ __forceinline__ i32x4 make_rsrc(const void* base, unsigned bytes) {
   return r;
 }
 
-template <typename T, int KIND>
+// XS = 1: the bf16x3 (fp32-class) network.  An fp32 activation row of C channels is stored as
+// [hi(C) | lo(C)] bf16 (hi = bf16(v), lo = bf16(v - hi)), and every input segment of C channels
+// is walked as 3 x C/KC chunks: (a_hi, w_hi), (a_hi, w_lo), (a_lo, w_hi) -- the same bf16 MFMA
+// loop over three times the chunks, fp32 accumulation (lo x lo, about 2^-16 relative, dropped).
+template <typename T, int KIND, int XS = 0>
 struct DmaPlan {
   using G = ConvGeom<T, KIND>;
+  static constexpr int X3 = XS ? 3 : 1, RS = XS ? 2 : 1;   // chunk multiplicity, row-stride factor
   i32x4 rs1, rs2, rsw;                // buffer resources: src1, src2, packed weights
+  int nc1 = 0, nc2 = 0, cc1 = 0, cc2 = 0;   // XS: chunks per plane and channels of both segments
   int avoff1[G::APT], avoff2[G::APT]; // byte offsets of this lane's A pieces (chunk 0) in src1 / src2
   int avoffh[G::APT2 > 0 ? G::APT2 : 1];  // fused segment 2: A pieces of the coarse input (src2)
   int bvoff;                          // byte offset of this lane's B piece 0 within a chunk's B tile
   int n1, wv, wbase;                  // wbase: byte offset of this tile's chunk 0 in the packed weights
 
   __device__ __forceinline__ void init(const ConvArgs<T>& a, int m0, int n_tile, int NC, int wv_, int lane) {
-    n1 = a.c1 / G::KC;
+    n1 = X3 * (a.c1 / G::KC);
+    if constexpr (XS != 0) {
+      nc1 = a.c1 / G::KC;
+      nc2 = a.c2 / G::KC;
+      cc1 = a.c1;
+      cc2 = a.c2;
+    }
     wv = wv_;
     const unsigned rows = (unsigned)a.B * G::LIN;
     const unsigned rows2 = G::FUSED ? (unsigned)a.B * G::LH : rows;
-    rs1 = make_rsrc(a.src1, rows * (unsigned)a.c1 * (unsigned)sizeof(T));
-    rs2 = make_rsrc(a.src2 ? a.src2 : a.src1, rows2 * (unsigned)a.c2 * (unsigned)sizeof(T));
+    rs1 = make_rsrc(a.src1, rows * (unsigned)(RS * a.c1) * (unsigned)sizeof(T));
+    rs2 = make_rsrc(a.src2 ? a.src2 : a.src1, rows2 * (unsigned)(RS * a.c2) * (unsigned)sizeof(T));
     const int tile_bytes = G::FUSED ? n1 * G::B_BYTES + (NC - n1) * G::B2_BYTES : NC * G::B_BYTES;
     rsw = make_rsrc(a.wpack, (unsigned)(a.cout / G::NT) * (unsigned)tile_bytes);
 #pragma unroll
@@ -470,8 +482,8 @@ struct DmaPlan {
       const int q1 = row / G::S;                 // fused: slot1 position index
       const int li = G::FUSED ? (q1 < G::LH ? 2 * q1 : 2 * (q1 - G::LH) + 1) : G::PM ? q1 : row - s * G::LIN;
       const int b = min(m0 + s, a.B - 1);        // rows of absent samples only feed unstored outputs
-      avoff1[qq] = ((b * G::LIN + li) * a.c1 + c * G::EPC) * (int)sizeof(T);
-      avoff2[qq] = ((b * G::LIN + li) * a.c2 + c * G::EPC) * (int)sizeof(T);
+      avoff1[qq] = ((b * G::LIN + li) * RS * a.c1 + c * G::EPC) * (int)sizeof(T);
+      avoff2[qq] = ((b * G::LIN + li) * RS * a.c2 + c * G::EPC) * (int)sizeof(T);
     }
     if constexpr (G::FUSED) {
 #pragma unroll
@@ -482,11 +494,21 @@ struct DmaPlan {
         const int c = cp ^ G::key(row);
         const int s = row % G::S, li = row / G::S;
         const int b = min(m0 + s, a.B - 1);
-        avoffh[qq] = ((b * G::LH + li) * a.c2 + c * G::EPC) * (int)sizeof(T);
+        avoffh[qq] = ((b * G::LH + li) * RS * a.c2 + c * G::EPC) * (int)sizeof(T);
       }
     }
     bvoff = (wv * 64 + lane) * 16;
     wbase = n_tile * tile_bytes;
+  }
+
+  // element offset within an input row of chunk k of a segment (nc chunks per plane, c channels)
+  __device__ __forceinline__ int coff(int k, int nc, int c) const {
+    if constexpr (XS != 0) {
+      const int g = (k >= nc) + (k >= 2 * nc);        // 0: a_hi, 1: a_hi again, 2: a_lo
+      return (k - g * nc) * G::KC + (g == 2 ? c : 0);
+    } else {
+      return k * G::KC;
+    }
   }
 
   // pieces per wave of chunk kc (fused: segment 2 chunks differ)
@@ -504,7 +526,7 @@ struct DmaPlan {
         const int p0 = k * kThreads + wv * 64;
         if (G::AFULL2 || p0 + lane < G::APIECES2)
           llvm_amdgcn_raw_buffer_load_lds(rs2, (__attribute__((address_space(3))) void*)(sbase + p0 * 16), 16,
-                                          avoffh[k], k2 * G::KC * (int)sizeof(T), 0, 0);
+                                          avoffh[k], coff(k2, nc2, cc2) * (int)sizeof(T), 0, 0);
       } else {
         const int qq = k - G::APT2;
         const int p0 = qq * kThreads + wv * 64;
@@ -521,7 +543,7 @@ struct DmaPlan {
       if (G::AFULL || p0 < G::APIECES) {
         if (G::AFULL || p0 + lane < G::APIECES) {
           const bool first = kc < n1;
-          const int soff = (first ? kc : kc - n1) * G::KC * (int)sizeof(T);
+          const int soff = coff(first ? kc : kc - n1, first ? nc1 : nc2, first ? cc1 : cc2) * (int)sizeof(T);
           llvm_amdgcn_raw_buffer_load_lds(first ? rs1 : rs2, (__attribute__((address_space(3))) void*)(sbase + p0 * 16),
                                           16, first ? avoff1[k] : avoff2[k], soff, 0, 0);
         }
@@ -582,6 +604,17 @@ template <> struct Vec8<bf16> {
     for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
     store16(reinterpret_cast<bf16x8*>(p), o);
   }
+  // bf16x3 network: hi = bf16(v) at p, lo = bf16(v - hi) at p + C
+  static __device__ __forceinline__ void store_split(bf16* p, int C, const float* v) {
+    bf16x8 o, r;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o[e] = (bf16)v[e];
+      r[e] = (bf16)(v[e] - (float)o[e]);
+    }
+    store16(reinterpret_cast<bf16x8*>(p), o);
+    store16(reinterpret_cast<bf16x8*>(p + C), r);
+  }
 };
 template <> struct Vec8<f16> {
   static __device__ __forceinline__ void store(f16* p, const float* v) {
@@ -590,17 +623,26 @@ template <> struct Vec8<f16> {
     for (int e = 0; e < 8; ++e) o[e] = (f16)v[e];
     store16(reinterpret_cast<f16x8*>(p), o);
   }
+  static __device__ __forceinline__ void store_split(f16*, int, const float*) {}
 };
 template <> struct Vec8<float> {
   static __device__ __forceinline__ void store(float* p, const float* v) {
     *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
     *reinterpret_cast<f32x4*>(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
   }
+  static __device__ __forceinline__ void store_split(float*, int, const float*) {}
 };
+
+// 8 channels n .. n+7 of activation row `row` of a C-channel tensor (XS: [hi | lo] rows of 2C)
+template <typename T, int XS>
+__device__ __forceinline__ void store_act(T* base, size_t row, int C, int n, const float* v) {
+  if constexpr (XS != 0) Vec8<T>::store_split(base + row * 2 * C + n, C, v);
+  else Vec8<T>::store(base + row * C + n, v);
+}
 
 // down0 positions pos0, pos0 + pstride, ... of samples b0 .. b0 + nb - 1: x from LDS
 // (xs [nb][96]), maps from LDS (mp [48][128], fast) or global, weights in registers.
-template <typename T>
+template <typename T, int XS = 0>
 __device__ __forceinline__ void down0_positions(const Down0Args& a, const float* xs, const float* mp, bool fast,
                                                 int b0, int nb, const f32x4 (&wr)[12][2], int n0, int pos0,
                                                 int pstride) {
@@ -645,13 +687,13 @@ __device__ __forceinline__ void down0_positions(const Down0Args& a, const float*
         v[e][q] = fmaxf(acc0[q] + m0[q], 0.f);
         v[e][4 + q] = fmaxf(acc1[q] + m1[q], 0.f);
       }
-      if constexpr (!(FIN_EXP & 2)) Vec8<T>::store(reinterpret_cast<T*>(a.s0) + ((size_t)b * 48 + l) * 128 + n0, v[e]);
+      if constexpr (!(FIN_EXP & 2)) store_act<T, XS>(reinterpret_cast<T*>(a.s0), (size_t)b * 48 + l, 128, n0, v[e]);
       else if (v[e][0] == 12345.f) reinterpret_cast<T*>(a.s0)[0] = (T)0.f;
     }
     float pv[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) pv[q] = fmaxf(v[0][q], v[1][q]);
-    if constexpr (!(FIN_EXP & 2)) Vec8<T>::store(reinterpret_cast<T*>(a.p0) + ((size_t)b * 24 + lp) * 128 + n0, pv);
+    if constexpr (!(FIN_EXP & 2)) store_act<T, XS>(reinterpret_cast<T*>(a.p0), (size_t)b * 24 + lp, 128, n0, pv);
     else if (pv[0] == 12345.f) reinterpret_cast<T*>(a.p0)[0] = (T)0.f;
   }
 }
@@ -671,7 +713,7 @@ __device__ __forceinline__ void ring_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <typename T, int KIND>
+template <typename T, int KIND, int XS = 0>
 __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvArgs<T> a) {
   using G = ConvGeom<T, KIND>;
   constexpr int L = G::L, TAPS = G::TAPS, PADL = G::PADL, EPI = G::EPI, ROWB = G::ROWB, NT = G::NT;
@@ -727,7 +769,7 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
 #endif
   const int m0 = m_tile * G::S;
 
-  const int NC = a.c1 / G::KC + a.c2 / G::KC;
+  const int NC = (XS ? 3 : 1) * (a.c1 / G::KC + a.c2 / G::KC);
 
   // Final level: this thread's output row (one per thread) and every global operand of its
   // p_sample, loaded at kernel start.  They are older than every LDS-DMA of the K loop, so the
@@ -839,7 +881,7 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][jn][e] = 0.f;
 
-  DmaPlan<T, KIND> dma;
+  DmaPlan<T, KIND, XS> dma;
   dma.init(a, m0, n_tile, NC, wv, lane);
 
   // One chunk: TAPS x (ROWB/32 bf16 | ROWB/64 f32) MFMA steps.  The DMA pieces of
@@ -887,7 +929,7 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
   for (int g = 0; g < NGE; ++g) epk[g][0] = epk[g][1] = fragT{};
   const char* ebase = nullptr;
   if constexpr (G::FUSED) {
-    const int n2 = a.c2 / G::KC;
+    const int n2 = (XS ? 3 : 1) * (a.c2 / G::KC);
     ebase = reinterpret_cast<const char*>(a.epack) +
             ((size_t)n_tile * n2 * 2 * NT + (size_t)ph * NT + wn * 64 + lr) * ROWB + h * 16;
   }
@@ -1625,7 +1667,7 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
 #pragma unroll
             for (int q = 0; q < 8; ++q) v[e][q] = fmaxf(v[e][q], 0.f);
           }
-          if (!FAST || be < B) Vec8<T>::store(a.out + ((size_t)be * L + le) * cout + n, v[e]);
+          if (!FAST || be < B) store_act<T, XS>(a.out, (size_t)be * L + le, cout, n, v[e]);
         }
       };
       if constexpr (G::PM && EPI == EPI_POOL) {
@@ -1643,7 +1685,7 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
             float pv[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) pv[q] = fmaxf(v0[e][q], v1[e][q]);
-            if (m0 + s + e < B) Vec8<T>::store(a.out_pool + ((size_t)(m0 + s + e) * (L / 2) + p) * cout + n, pv);
+            if (m0 + s + e < B) store_act<T, XS>(a.out_pool, (size_t)(m0 + s + e) * (L / 2) + p, cout, n, pv);
           }
         }
       } else {
@@ -1661,7 +1703,7 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
             float pv[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) pv[q] = fmaxf(v[0][q], v[1][q]);
-            if (!FAST || b < B) Vec8<T>::store(a.out_pool + ((size_t)b * (L / 2) + (l >> 1)) * cout + n, pv);
+            if (!FAST || b < B) store_act<T, XS>(a.out_pool, (size_t)b * (L / 2) + (l >> 1), cout, n, pv);
           }
         }
       }
@@ -1811,7 +1853,7 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
         for (int k = 0; k < 6; ++k) reinterpret_cast<f32x4*>(mp)[tid + kThreads * k] = mv[k];
       }
       __syncthreads();
-      if constexpr (!(FIN_EXP & 1)) down0_positions<T>(nd, xst, mp, fast, m0, nb_next, wr, n0_next, tid >> 4, kThreads / 16);
+      if constexpr (!(FIN_EXP & 1)) down0_positions<T, XS>(nd, xst, mp, fast, m0, nb_next, wr, n0_next, tid >> 4, kThreads / 16);
 #if CONV_EXP_MODE & 128
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -1825,7 +1867,7 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
 // down0 block: K = 6 taps x 2 x-channels (label/time folded into maps) -> VALU.
 // Writes the skip s0 (B*48 x 128) and the pooled p0 (B*24 x 128).
 // ---------------------------------------------------------------------------
-template <typename T>
+template <typename T, int XS = 0>
 __global__ __launch_bounds__(512) void down0_kernel(Down0Args a, int spb) {
   // One block per `spb` consecutive samples (<= 8).  The samples' x and the level's
   // time + label map row block (t uniform, one condition) are staged in LDS once and
@@ -1864,7 +1906,7 @@ __global__ __launch_bounds__(512) void down0_kernel(Down0Args a, int spb) {
     for (int k = 0; k < 3; ++k) reinterpret_cast<f32x4*>(mp)[tid + 512 * k] = mv[k];
   }
   __syncthreads();
-  down0_positions<T>(a, xs, mp, fast, b0, nb, wr, n0, tid >> 4, 32);
+  down0_positions<T, XS>(a, xs, mp, fast, b0, nb, wr, n0, tid >> 4, 32);
 }
 
 // ---------------------------------------------------------------------------
@@ -2070,10 +2112,19 @@ __global__ void to_f32_kernel(const T* src, size_t n, float* dst) {
   if (i < n) dst[i] = to_f(src[i]);
 }
 
+// bf16x3 activation rows [hi(C) | lo(C)] -> fp32 [rows][C]
+__global__ void split_to_f32_kernel(const bf16* src, size_t rows, int C, float* dst) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < rows * C) {
+    const size_t r = i / C, c = i - r * C;
+    dst[i] = (float)src[r * 2 * C + c] + (float)src[r * 2 * C + C + c];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
-template <typename T, int KIND>
+template <typename T, int KIND, int XS>
 static hipError_t launch_one(const ConvArgs<T>& a, hipStream_t s) {
   using G = ConvGeom<T, KIND>;
   if (a.B <= 0) return hipSuccess;
@@ -2081,45 +2132,61 @@ static hipError_t launch_one(const ConvArgs<T>& a, hipStream_t s) {
   if (G::FUSED && (!a.src2 || !a.epack || a.c2 <= 0)) return hipErrorInvalidValue;
   const int nM = (a.B + G::S - 1) / G::S;
   const int total = nM * (a.cout / G::NT);
-  hipLaunchKernelGGL((conv_kernel<T, KIND>), dim3(total), dim3(G::NTH), 0, s, a);
+  hipLaunchKernelGGL((conv_kernel<T, KIND, XS>), dim3(total), dim3(G::NTH), 0, s, a);
   return hipGetLastError();
 }
 
-template <typename T>
-hipError_t launch_conv(int kind, const ConvArgs<T>& a, hipStream_t s) {
+template <typename T, int XS>
+static hipError_t launch_conv_xs(int kind, const ConvArgs<T>& a, hipStream_t s) {
   switch (kind) {
-    case LK_DOWN1: return launch_one<T, LK_DOWN1>(a, s);
-    case LK_DOWN2: return launch_one<T, LK_DOWN2>(a, s);
-    case LK_DOWN3: return launch_one<T, LK_DOWN3>(a, s);
-    case LK_UP0_CONV2: return launch_one<T, LK_UP0_CONV2>(a, s);
-    case LK_UP0_BLOCK: return launch_one<T, LK_UP0_BLOCK>(a, s);
-    case LK_UP1_CONV2: return launch_one<T, LK_UP1_CONV2>(a, s);
-    case LK_UP1_BLOCK: return launch_one<T, LK_UP1_BLOCK>(a, s);
-    case LK_UP2_CONV2: return launch_one<T, LK_UP2_CONV2>(a, s);
-    case LK_UP2_BLOCK: return launch_one<T, LK_UP2_BLOCK>(a, s);
+    case LK_DOWN1: return launch_one<T, LK_DOWN1, XS>(a, s);
+    case LK_DOWN2: return launch_one<T, LK_DOWN2, XS>(a, s);
+    case LK_DOWN3: return launch_one<T, LK_DOWN3, XS>(a, s);
+    case LK_UP0_CONV2: return launch_one<T, LK_UP0_CONV2, XS>(a, s);
+    case LK_UP0_BLOCK: return launch_one<T, LK_UP0_BLOCK, XS>(a, s);
+    case LK_UP1_CONV2: return launch_one<T, LK_UP1_CONV2, XS>(a, s);
+    case LK_UP1_BLOCK: return launch_one<T, LK_UP1_BLOCK, XS>(a, s);
+    case LK_UP2_CONV2: return launch_one<T, LK_UP2_CONV2, XS>(a, s);
+    case LK_UP2_BLOCK: return launch_one<T, LK_UP2_BLOCK, XS>(a, s);
   }
   if constexpr (sizeof(T) == 2) {   // fused up levels: 16-bit MFMA path only
     switch (kind) {
-      case LK_UP0_F: return launch_one<T, LK_UP0_F>(a, s);
-      case LK_UP1_F: return launch_one<T, LK_UP1_F>(a, s);
-      case LK_UP2_F: return launch_one<T, LK_UP2_F>(a, s);
+      case LK_UP0_F: return launch_one<T, LK_UP0_F, XS>(a, s);
+      case LK_UP1_F: return launch_one<T, LK_UP1_F, XS>(a, s);
+      case LK_UP2_F: return launch_one<T, LK_UP2_F, XS>(a, s);
     }
   }
   return hipErrorInvalidValue;
 }
 
 template <typename T>
-hipError_t launch_down0(const Down0Args& a, hipStream_t s) {
+hipError_t launch_conv(int kind, const ConvArgs<T>& a, hipStream_t s, bool x3) {
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (x3) return launch_conv_xs<T, 1>(kind, a, s);
+  }
+  if (x3) return hipErrorInvalidValue;
+  return launch_conv_xs<T, 0>(kind, a, s);
+}
+
+template <typename T>
+hipError_t launch_down0(const Down0Args& a, hipStream_t s, bool x3) {
   if (a.B <= 0) return hipSuccess;
   // ~1 block per CU: spb samples per block (<= 8, the LDS x stage)
   const int spb = std::min(8, std::max(1, (a.B + 255) / 256));
-  hipLaunchKernelGGL(down0_kernel<T>, dim3((a.B + spb - 1) / spb), dim3(512), 0, s, a, spb);
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (x3) {
+      hipLaunchKernelGGL((down0_kernel<T, 1>), dim3((a.B + spb - 1) / spb), dim3(512), 0, s, a, spb);
+      return hipGetLastError();
+    }
+  }
+  if (x3) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((down0_kernel<T, 0>), dim3((a.B + spb - 1) / spb), dim3(512), 0, s, a, spb);
   return hipGetLastError();
 }
 
-template hipError_t launch_conv<bf16>(int, const ConvArgs<bf16>&, hipStream_t);
-template hipError_t launch_conv<f16>(int, const ConvArgs<f16>&, hipStream_t);
-template hipError_t launch_conv<float>(int, const ConvArgs<float>&, hipStream_t);
+template hipError_t launch_conv<bf16>(int, const ConvArgs<bf16>&, hipStream_t, bool);
+template hipError_t launch_conv<f16>(int, const ConvArgs<f16>&, hipStream_t, bool);
+template hipError_t launch_conv<float>(int, const ConvArgs<float>&, hipStream_t, bool);
 hipError_t launch_set_rng(unsigned long long* dst, unsigned long long seed, unsigned long long off0,
                           unsigned long long off1, int parts, hipStream_t s) {
   hipLaunchKernelGGL(set_rng_kernel, dim3(1), dim3(64), 0, s, dst, seed, off0, off1, parts);
@@ -2135,9 +2202,15 @@ hipError_t launch_to_f32(const T* src, size_t n, float* dst, hipStream_t s) {
 template hipError_t launch_to_f32<bf16>(const bf16*, size_t, float*, hipStream_t);
 template hipError_t launch_to_f32<f16>(const f16*, size_t, float*, hipStream_t);
 template hipError_t launch_to_f32<float>(const float*, size_t, float*, hipStream_t);
-template hipError_t launch_down0<bf16>(const Down0Args&, hipStream_t);
-template hipError_t launch_down0<f16>(const Down0Args&, hipStream_t);
-template hipError_t launch_down0<float>(const Down0Args&, hipStream_t);
+template hipError_t launch_down0<bf16>(const Down0Args&, hipStream_t, bool);
+template hipError_t launch_down0<f16>(const Down0Args&, hipStream_t, bool);
+template hipError_t launch_down0<float>(const Down0Args&, hipStream_t, bool);
+hipError_t launch_split_to_f32(const bf16* src, size_t rows, int C, float* dst, hipStream_t s) {
+  const size_t n = rows * (size_t)C;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(split_to_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, rows, C, dst);
+  return hipGetLastError();
+}
 
 hipError_t launch_time_emb(const float* w, const float* b, int T, int sin_dim, int hid, float* out,
                            hipStream_t s) {

@@ -139,7 +139,9 @@ class ImprovedDDPM:
 
         self.dtype = {'bfloat16': _lib.DTYPE_BF16, 'bf16': _lib.DTYPE_BF16,
                       'float16': _lib.DTYPE_F16, 'fp16': _lib.DTYPE_F16, 'half': _lib.DTYPE_F16,
-                      'float32': _lib.DTYPE_F32, 'fp32': _lib.DTYPE_F32}[str(dtype)]
+                      'float32': _lib.DTYPE_F32, 'fp32': _lib.DTYPE_F32,
+                      # fp32-class accuracy on the bf16 MFMA path (hi/lo split, 3 products; petdiff.h)
+                      'bf16x3': _lib.DTYPE_BF16X3}[str(dtype)]
         if device is None:
             device = torch.cuda.current_device() if torch.cuda.is_available() else 0
         self.device = torch.device('cuda', device if isinstance(device, int) else torch.device(device).index or 0)
