@@ -450,7 +450,7 @@ def bf16x3_rate(cond, B, n_rev, dev):
 
 
 def mh_slice_and_protocol(iddpm_10k_s, dev):
-    """BASELINE configs[2] slice (10k chains x 500 steps of the 20k) and the reference's per-TAC
+    """BASELINE configs[2] slice (10k chains x 2000 steps of the 20k) and the reference's per-TAC
     MCMC protocol (main_script.py:363-364, pymc's default 4 chains: 4 x (20k draws + 40k tune)),
     timed as a 1/10 slice x 10; ratio against iDDPM's 10,000 posterior samples of one TAC
     (main_script.py:315-319) on the same GPU -- the README.md:12 '> 230x' claim, same silicon."""
@@ -460,7 +460,7 @@ def mh_slice_and_protocol(iddpm_10k_s, dev):
     mh = MetropolisSRTM2(**mh_problem(seed=0))
     mh.run(512, 2, 0, seed=1)
     torch.cuda.synchronize()
-    n, tune, draws = 10000, 250, 250
+    n, tune, draws = 10000, 1000, 1000      # about 1.6 s: long enough that run set-up is < 2 %
     t0 = time.perf_counter()
     res = mh.run(n, draws, tune, seed=7)
     torch.cuda.synchronize()

@@ -68,3 +68,21 @@ def test_max_batch_constant_matches_header():
     txt = open(os.path.join(ROOT, 'include', 'petdiff.h')).read()
     m = re.search(r'#define\s+PETDIFF_MAX_BATCH\s+(\d+)', txt)
     assert m and int(m.group(1)) == _lib.MAX_BATCH
+
+
+def test_dtype_constants_match_header():
+    """_lib's dtype codes (incl. the bf16x3 network) are the header's PETDIFF_DTYPE_* values, and
+    petdiff_create rejects an unknown dtype before touching the device."""
+    from pet_posterior_distribution_amd import _lib
+    txt = open(os.path.join(ROOT, 'include', 'petdiff.h')).read()
+    hdr = {k: int(v) for k, v in re.findall(r'#define\s+PETDIFF_DTYPE_(\w+)\s+(\d+)', txt)}
+    assert hdr == {'F32': _lib.DTYPE_F32, 'BF16': _lib.DTYPE_BF16, 'F16': _lib.DTYPE_F16,
+                   'BF16X3': _lib.DTYPE_BF16X3}
+    L = _lib.lib()
+    cfg = _lib.PetdiffConfig()
+    assert L.petdiff_default_config(C.byref(cfg)) == 0
+    cfg.dtype = 7
+    h = C.c_void_p()
+    w = np.zeros(_lib.lib().petdiff_param_count(C.byref(cfg)), np.float32)
+    rc = L.petdiff_create(C.byref(cfg), w.ctypes.data_as(C.c_void_p), w.size, 0, C.byref(h))
+    assert rc == _lib.PETDIFF_ERR_INVALID and 'PETDIFF_DTYPE_BF16X3' in _lib.last_error()
