@@ -117,3 +117,19 @@ def test_config2_full_size_bf16x3_vs_f32(trained, trained_x3):
     g = trained_x3.ddpm_loop(x[:64], cond[None], num_timesteps=40, seed=9)
     torch.testing.assert_close(e, g, rtol=0, atol=0)
     f32.close()
+
+
+def test_loop_mixed_conditions_per_sample_bf16x3(trained, trained_x3):
+    """Conditions interleaved per sample (the epilogues' per-row map path) through the loop with
+    injected noise vs the fp64 oracle, 1e-4 of max|oracle|."""
+    W, cond = trained
+    rng = np.random.default_rng(21)
+    B = 40
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    table = np.stack([cond, synthetic_condition(1), cond * 0.9 + 0.05])
+    tac = rng.integers(0, 3, B).astype(np.int32)
+    idx = R.loop_indices(1000, 12)
+    z = rng.standard_normal((len(idx), B, 48, 2)).astype(np.float32)
+    out = trained_x3.ddpm_loop(x, table, num_timesteps=12, z=z, tac=tac).cpu().numpy()
+    ref = R.ddpm_loop(W, S, x, table[tac], z, idx, dt=np.float64)
+    assert np.abs(out - ref).max() <= 1e-4 * np.abs(ref).max()

@@ -344,7 +344,7 @@ def test_loop_tac_major_graph_bf16(m16, conds):
     torch.testing.assert_close(both, torch.cat([a, b]), rtol=0, atol=0)
 
 
-@pytest.mark.parametrize('dtype', ['bfloat16', 'float32'])
+@pytest.mark.parametrize('dtype', ['bfloat16', 'float32', 'bf16x3'])
 def test_fused_next_step_down0_bitwise(conds, dtype, monkeypatch):
     """The loop runs step i+1's first layer (down0) inside step i's final-conv epilogue;
     PETDIFF_FUSE_DOWN0=0 keeps the standalone down0 launch.  Same arithmetic either way:
