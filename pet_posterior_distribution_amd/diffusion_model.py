@@ -17,8 +17,11 @@ tfunc_ddpm_loop         :718-737       ``tfunc_ddpm_loop`` (hipGraph replay)
 
 Inputs may be NumPy arrays or torch tensors; outputs are torch tensors on the
 sampler's GPU (``keep_all_xt`` returns a NumPy stack, as the reference does at
-:712-713).  The network runs in ``dtype`` ('bfloat16' by default, or 'float32'
-for the exact-f32 MFMA parity mode); the p_sample epilogue is always fp32.
+:712-713).  The network runs in ``dtype``: 'bf16x3' by default -- the reference's fp32
+accuracy (1e-4 parity) on the bf16 MFMA kernels, every fp32 operand split hi + lo and
+three bf16 products per fp32 product -- or 'bfloat16' / 'float16' (the benchmarked
+16-bit networks, about 2.4x faster) or 'float32' (exact-f32 MFMA, 3.7x slower than
+'bf16x3'); the p_sample epilogue is always fp32.
 
 Noise: the reference draws ``tf.random.normal`` from TF's stateful Philox.  Here
 z is a counter-based Philox4x32-10 normal keyed by (seed, global sample index,
@@ -82,7 +85,7 @@ class ImprovedDDPM:
     v_param_name_list = ['v', ]
 
     def __init__(self, lambda_vlb=0.1, parameterization='eps', timesteps=200, noise_schedule=None,
-                 network=None, ndim=None, constrained_func_output_t0=None, dtype='bfloat16', device=None,
+                 network=None, ndim=None, constrained_func_output_t0=None, dtype='bf16x3', device=None,
                  seed=12345, **kwargs):
         # ---- DDPM.__init__ (diffusion_model.py:79-135) ----
         self.timesteps = timesteps
