@@ -6,7 +6,8 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $OUT
-APP="python $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --reverse-steps 20 --no-cpu-baseline --no-kernel-timing"
+# BENCH_EXTRA: more bench.py flags, e.g. "--dtype bf16x3"
+APP="python $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --reverse-steps 20 --no-cpu-baseline --no-kernel-timing ${BENCH_EXTRA}"
 i=0
 for CTR in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_LDS_UNALIGNED_STALL"; do
   i=$((i+1))
