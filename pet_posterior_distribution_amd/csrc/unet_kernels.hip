@@ -85,6 +85,16 @@
 #ifndef CONV_DOWN2_PM
 #define CONV_DOWN2_PM 1
 #endif
+// down1 (L = 24, 16 samples per tile) pair-position-major: fragment F = positions 2F, 2F + 1 of the
+// tile's 16 samples (lanes 0-15 / 16-31), LDS input slots position-major (p * 16 + s).  A lane
+// group of 16 then reads 16 consecutive slots, or (tap outside the sample) the zero row as a
+// broadcast, instead of sample-major rows broken by zero-row substitutions (LDS bank conflicts).
+// The K walk per output row is unchanged, so the results are bitwise those of sample-major rows.
+// Measured and off: LDS bank conflicts 442 k -> 111 k (-> 307 k with the
+// sample-major C-tile remap below) per launch, but down1 14.65 vs 14.50 us, 0.9 % slower end to end.
+#ifndef CONV_DOWN1_PP
+#define CONV_DOWN1_PP 0
+#endif
 
 namespace petdiff {
 
@@ -276,6 +286,8 @@ struct ConvGeom {
   //   down2 (L = 12, S = 32): {0, 2, 3}, {10, 4, 5}, {1, 9, 6} keep 16, {11, 7, 8} 15.
   static constexpr bool PM = sizeof(T) == 2 && ((CONV_DOWN3_PM && KIND == LK_DOWN3) ||
                                                 (CONV_DOWN2_PM && KIND == LK_DOWN2));
+  static constexpr bool PP = sizeof(T) == 2 && CONV_DOWN1_PP && KIND == LK_DOWN1;
+  static constexpr bool POSMAJ = PM || PP;          // LDS input slots p * S + s
   static constexpr int SH = PM ? S / 32 : 1;        // sample halves (waves per fragment set)
   static constexpr int NPAT = 4 / SH;               // fragment sets
   // fragment set pat, fragment i -> position, packed 4 bits per entry (index 3 pat + i), so a
@@ -377,6 +389,8 @@ struct ConvGeom {
                 "position-major layout: 3 positions of 32 samples per wave");
   static_assert(!PM || (CONV_LOADERS && STAGES == 3), "position-major layers run on the loader-wave ring");
   static_assert(MT % L == 0, "tile must hold whole samples");
+  static_assert(!PP || (S == 16 && L % 2 == 0 && MT == 32 * (L / 2) && !UPS && !FUSED && EPI == EPI_POOL),
+                "pair-position-major: a fragment is two positions of 16 samples");
   static_assert(B_BYTES % (16 * kThreads) == 0, "B tile split");
   static_assert(ROWB == 64 || ROWB == 128 || (ROWB == 32 && FUSED), "row width");
   static_assert(STAGES == 2 || (STAGES == 3 && AFULL && AFULL2), "3-stage ring needs uniform per-wave DMA counts");
@@ -478,9 +492,9 @@ struct DmaPlan {
       const int c = cp ^ G::key(row);
       // LDS row: (sample, position) = row / LIN, row % LIN; fused: position-major slots
       // (row = li * S + s), so a lane group's 16 samples read 16 consecutive rows
-      const int s = (G::FUSED || G::PM) ? row % G::S : row / G::LIN;
+      const int s = (G::FUSED || G::POSMAJ) ? row % G::S : row / G::LIN;
       const int q1 = row / G::S;                 // fused: slot1 position index
-      const int li = G::FUSED ? (q1 < G::LH ? 2 * q1 : 2 * (q1 - G::LH) + 1) : G::PM ? q1 : row - s * G::LIN;
+      const int li = G::FUSED ? (q1 < G::LH ? 2 * q1 : 2 * (q1 - G::LH) + 1) : G::POSMAJ ? q1 : row - s * G::LIN;
       const int b = min(m0 + s, a.B - 1);        // rows of absent samples only feed unstored outputs
       avoff1[qq] = ((b * G::LIN + li) * RS * a.c1 + c * G::EPC) * (int)sizeof(T);
       avoff2[qq] = ((b * G::LIN + li) * RS * a.c2 + c * G::EPC) * (int)sizeof(T);
@@ -826,13 +840,16 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
       if constexpr (G::PM) {   // wave-uniform position: scalar work, no divergent select chain
         l = G::pm_pos(pm_pat, i);
         s = (wv % G::SH) * 32 + lr;
+      } else if constexpr (G::PP) {   // fragment rows: positions 2F (lanes 0-15), 2F + 1 (16-31)
+        l = 2 * (r >> 5) + ((r >> 4) & 1);
+        s = r & 15;
       } else {
         G::row_sl(r, s, l);
       }
       const int p = l + j - PADL;
       int row;
       if (G::FUSED) row = (p >= 0 && p < L) ? G::slot1(p, s) : G::ZROW;
-      else if (!UPS) row = (p >= 0 && p < L) ? (G::PM ? p * G::S + s : s * L + p) : G::ZROW;
+      else if (!UPS) row = (p >= 0 && p < L) ? (G::POSMAJ ? p * G::S + s : s * L + p) : G::ZROW;
       else row = (p < L) ? s * G::LIN + (p >> 1) : G::ZROW;
       aoff[j][i] = (G::FUSED && row == G::ZROW) ? G::ZOFF + (c0 << 4) : row * ROWB + ((c0 ^ G::key(row)) << 4);
     }
@@ -1598,6 +1615,22 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
     // The tile interleaves row pairs ([r/2][c][2]): an accumulator's consecutive rows
     // (rg, rg+1) go out as one ds_write_b64 and a row pair comes back as 4 ds_read_b128.
     float* ct = reinterpret_cast<float*>(smem);
+    if constexpr (G::PP) {
+      // pair-position-major fragments: accumulator rows rg < 8 are position 2F of sample s, rg + 8
+      // the same sample at 2F + 1 -- written as the sample-major row pair, so the epilogue below
+      // (pooled pairs = two positions of one sample) is the sample-major one
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+          for (int rg = 0; rg < 8; ++rg) {
+            const int r = wm * 96 + i * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * h;   // bit 4 clear
+            const int rs = (r & 15) * L + 2 * (r >> 5);                           // (s, 2F): even
+            *reinterpret_cast<float2*>(ct + (rs >> 1) * G::CT_LD + (wn * 64 + jn * 32 + lr) * 2) =
+                make_float2(acc[i][jn][rg], acc[i][jn][rg + 8]);
+          }
+    } else
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll

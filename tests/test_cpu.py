@@ -378,3 +378,40 @@ def test_torch_cpu_baseline_port_matches_oracle():
     for a, b in ((m, m_ref), (vt, vt_ref)):
         a = a.numpy()
         assert np.abs(a - b).max() <= 2e-5 * max(1.0, np.abs(b).max()), np.abs(a - b).max()
+
+
+def test_down1_pair_position_major_layout():
+    """down1's pair-position-major tile (CONV_DOWN1_PP, unet_kernels.hip): fragment F of the 384-row
+    tile holds positions 2F (lanes 0-15) and 2F+1 (lanes 16-31) of the tile's 16 samples, the LDS
+    input slots are position-major (p * 16 + s), and the C tile is written back as sample-major row
+    pairs.  Checks, in the kernel's integer arithmetic: every (sample, position) is one tile row;
+    a 16-lane group reads 16 consecutive slots or only the zero row for every tap; the accumulator
+    row pairs (rg, rg + 8), rg < 8, land on each sample-major pair (s, 2F | 2F + 1) exactly once."""
+    L, S, MT = 24, 16, 384
+    seen = set()
+    for r in range(MT):
+        l, s = 2 * (r >> 5) + ((r >> 4) & 1), r & 15
+        seen.add((s, l))
+    assert seen == {(s, l) for s in range(S) for l in range(L)}
+    ZROW = S * L
+    for F in range(MT // 32):
+        for j in range(6):
+            for g in range(2):
+                slots = []
+                for lr in range(16 * g, 16 * g + 16):
+                    r = 32 * F + lr
+                    l, s = 2 * (r >> 5) + ((r >> 4) & 1), r & 15
+                    p = l + j - 2
+                    slots.append(p * S + s if 0 <= p < L else ZROW)
+                assert slots == [ZROW] * 16 or slots == list(range(slots[0], slots[0] + 16))
+    pairs = []
+    for wm in range(4):
+        for i in range(3):
+            for h in range(2):
+                for rg in range(8):
+                    r = wm * 96 + i * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * h
+                    assert r & 16 == 0
+                    r2 = r + 16        # accumulator element rg + 8 of the same lane
+                    assert (r2 & 15, 2 * (r2 >> 5) + ((r2 >> 4) & 1)) == (r & 15, 2 * (r >> 5) + 1)
+                    pairs.append(((r & 15) * L + 2 * (r >> 5)) >> 1)
+    assert sorted(pairs) == list(range(MT // 2))
