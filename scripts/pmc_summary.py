@@ -29,7 +29,7 @@ def short(name):
     return None
 
 
-def main(d, out=None):
+def main(d, out=None, update_traffic=False):
     vals = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(d, 'p*', 'run_counter_collection.csv')):
         for r in csv.DictReader(open(f)):
@@ -48,6 +48,9 @@ def main(d, out=None):
         print(k, {c: round(v, 1) for c, v in res[k].items()})
     if out:
         json.dump(res, open(out, 'w'), indent=1)
+    if out and update_traffic:
+        # bench.py's bf16 roofline reads these: update them only from passes over the default
+        # (bf16, B = 1024) workload -- a --dtype bf16x3 run once overwrote them with its 3x bytes
         root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
         tp = os.path.join(root, 'profiles', 'pmc_traffic.json')
         tr = json.load(open(tp)) if os.path.exists(tp) else {}
@@ -67,4 +70,5 @@ def main(d, out=None):
 
 
 if __name__ == '__main__':
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
+    args = [x for x in sys.argv[1:] if x != '--traffic']
+    main(args[0], args[1] if len(args) > 1 else None, update_traffic='--traffic' in sys.argv[1:])

@@ -415,3 +415,14 @@ def test_down1_pair_position_major_layout():
                     assert (r2 & 15, 2 * (r2 >> 5) + ((r2 >> 4) & 1)) == (r & 15, 2 * (r >> 5) + 1)
                     pairs.append(((r & 15) * L + 2 * (r >> 5)) >> 1)
     assert sorted(pairs) == list(range(MT // 2))
+
+
+def test_bench_pmc_fields_are_bf16_passes():
+    """bench.py's roofline traffic / MFMA-busy fields (bf16 line) come from profiles/pmc_traffic.json;
+    they must be passes over the bf16 network: SQ_VALU_MFMA_BUSY_CYCLES of up0.fused equals the
+    analytic executed count (32 busy cycles per 32x32x16 MFMA of 32,768 FLOP), not bf16x3's 3x."""
+    import bench
+    pmc = bench.load_pmc(True)
+    want = bench.UP0_FUSED_EXEC_FLOP_PER_SAMPLE * 1024 / 32768 * 32
+    assert pmc['mfma_busy'] is not None and abs(pmc['mfma_busy'] / want - 1) < 0.01
+    assert pmc['traffic'] is not None and pmc['traffic'] < 2.5e8
