@@ -92,6 +92,17 @@
 // The K walk per output row is unchanged, so the results are bitwise those of sample-major rows.
 // Measured and off: LDS bank conflicts 442 k -> 111 k (-> 307 k with the
 // sample-major C-tile remap below) per launch, but down1 14.65 vs 14.50 us, 0.9 % slower end to end.
+// up0 fused level (tap reuse path, S = 32): a fragment is one coarse row m of 32 samples, so the
+// m = 0 fragment's composite tap 0 reads coarse row -1, the zero row.  1 = the waves holding m = 0
+// run their left-edge correction MFMAs (b[0] x correction weights) in place of those zero-operand
+// tap-0 MFMAs (operands selected per wave), instead of 2 extra MFMAs per k-group: 52 -> 48 MFMAs per
+// segment-2 chunk on those waves, the same 48 as the other waves (0 = separate correction MFMAs).
+// Measured and off (profiles/r02/ab/up0_edge_tap0): up0.fused 72.40 vs 72.29 us, 4538 vs 4545
+// samples/s, 8 % more active instructions (the operand selects); not bitwise equal (the correction
+// of k-group 1 is added 4 steps later), within rounding of it.
+#ifndef CONV_UP0_EDGE_TAP0
+#define CONV_UP0_EDGE_TAP0 0
+#endif
 #ifndef CONV_DOWN1_PP
 #define CONV_DOWN1_PP 0
 #endif
@@ -977,6 +988,9 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
       static_assert(NS % 2 == 0, "B double buffer alternates per step");
       fragT AP[NG][NPOS];
       fragT am[SEG == 2 ? NG : 1];
+      // edge correction folded into tap 0 (CONV_UP0_EDGE_TAP0): am is read by every wave (the zero
+      // row where no m = 0 rows), so the per-wave operand select never sees an undefined value
+      constexpr bool ETAP0 = CONV_UP0_EDGE_TAP0 && SEG == 2;
       // LDS offset of relative position P (any (tap, fragment) pair that lands on it)
       auto posoff = [&](int P) -> int {
         if constexpr (SEG == 2) {
@@ -1003,8 +1017,12 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
           pb1 = base + ((boff2[1] + j * NT * ROWB) ^ (g << 5));
         }
 #define PETDIFF_RMF(i, jn)                                                                                 \
-  if constexpr (!(CONV_EXP_MODE & 2))                                                                      \
-    acc[i][jn] = mfma32(st == 0 ? cav[i] : AP[gp][jp + D * (i)], bv[pb][jn], acc[i][jn]);
+  if constexpr (!(CONV_EXP_MODE & 2)) {                                                                    \
+    if (ETAP0 && (i) == 0 && st > 0 && jp == 0)                                                            \
+      acc[0][jn] = mfma32(has_m0 ? am[gp] : AP[gp][0], has_m0 ? epk[gp][jn] : bv[pb][jn], acc[0][jn]);    \
+    else                                                                                                   \
+      acc[i][jn] = mfma32(st == 0 ? cav[i] : AP[gp][jp + D * (i)], bv[pb][jn], acc[i][jn]);                \
+  }
 #define PETDIFF_RRD(dst, off) \
   if constexpr (!(CONV_EXP_MODE & 64)) dst = *reinterpret_cast<const fragT*>(base + ((off) ^ (g << 5)));
 #define PETDIFF_BRD(dst, ptr) \
@@ -1045,7 +1063,17 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
 #undef PETDIFF_BRD
 #undef PETDIFF_RRD
 #undef PETDIFF_RMF
-        if constexpr (SEG == 2) {
+        if constexpr (ETAP0) {
+          if (st == 0) {
+#pragma unroll
+            for (int gg = 0; gg < NG; ++gg) am[gg] = *reinterpret_cast<const fragT*>(base + (amask ^ (gg << 5)));
+          }
+          // the last k-group's tap-0 MFMAs (step (NG - 1) NT_, issued at the step after it) use epk
+          if (st == (NG - 1) * NT_ + 1 && has_m0) {
+            const int k2 = kc - dma.n1;
+            if (kc + 1 < NC) load_epk(k2 + 1);
+          }
+        } else if constexpr (SEG == 2) {
           if (st == 0 && has_m0) {
 #pragma unroll
             for (int gg = 0; gg < NG; ++gg) am[gg] = *reinterpret_cast<const fragT*>(base + (amask ^ (gg << 5)));
