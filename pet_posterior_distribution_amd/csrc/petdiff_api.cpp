@@ -152,6 +152,9 @@ struct petdiff_ctx {
   // run the next step's down0 inside the previous step's up2.block epilogue (generate);
   // PETDIFF_FUSE_DOWN0=0 restores the standalone down0 launch per step (A/B switch)
   bool fuse_down0 = true;
+  // ... and the next step's down1 too (bf16, one condition; PETDIFF_FUSE_DOWN1=1).  Off: measured
+  // slower than the standalone launch (unet_kernels.hip, fused_down1)
+  bool fuse_down1 = false;
   DevBuf xa, xb, tacbuf, tbuf, rng;
   hipStream_t cap_stream = nullptr;
   hipStream_t split_stream = nullptr;  // second launch stream of a split generate (PETDIFF_SPLIT)
@@ -388,6 +391,7 @@ struct StepIO {
   FinalArgs fin;
   int s0_sel;                 // skip buffer of this step: 0 -> s0, 1 -> s0b
   bool skip_down0;            // s0/p0 already written by the previous step's fused epilogue
+  bool d1_ok;                 // generate: the fused epilogue may also run the next step's down1
   bool fuse_next;             // up2.block epilogue also runs down0 of the next step (t = next_t)
   int next_t;
   int b_off;                  // first sample of this launch inside the workspace (split streams)
@@ -441,6 +445,8 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
   d0.p0 = p0;
   d0.B = B;
   if (!io.skip_down0) CHK(timed(0, [&] { return launch_down0<T>(d0, s, h->x3); }));
+  // fused down1 (16-bit bf16 network, one condition): the previous step's epilogue wrote s1 / p1
+  const bool d1_fuse = io.d1_ok && std::is_same<T, bf16>::value && !h->x3 && h->fuse_up && io.tac == nullptr;
 
   struct LIO { const void* s1; int c1; const void* s2; int c2; void* out; void* pool; };
   const LIO lio[kNumConvLayers] = {
@@ -489,11 +495,20 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
           a.fin.next.tvec = nullptr;
           a.fin.next.t_uniform = io.next_t;
           a.fin.next.s0 = s0_other;
+          if (d1_fuse) {   // s1 / p1 are dead once up1 and down2 of this step have run
+            const int lv = kConv[LK_DOWN1].cond_level;
+            a.fin.d1_w = h->wpack[LK_DOWN1].p;
+            a.fin.d1_tmap = h->tmap[lv].as<float>();
+            a.fin.d1_cmap = h->cmap[lv].as<float>();
+            a.fin.d1_s1 = s1;
+            a.fin.d1_p1 = p1;
+          }
         }
       }
       CHK(timed(1 + li, [&] { return launch_conv<T>(fl.kind, a, s, h->x3); }));
       continue;
     }
+    if (li == LK_DOWN1 && d1_fuse && io.skip_down0) continue;   // done by the previous step's epilogue
     ConvArgs<T> a{};
     a.src1 = reinterpret_cast<const T*>(lio[li].s1);
     a.c1 = lio[li].c1;
@@ -630,6 +645,7 @@ int petdiff_create(const petdiff_config* cfg, const float* weights, size_t n_wei
   h->x3 = cfg->dtype == PETDIFF_DTYPE_BF16X3;
   h->spec = make_spec(*cfg, h->n_out);
   if (const char* e = std::getenv("PETDIFF_FUSE_DOWN0")) h->fuse_down0 = std::atoi(e) != 0;
+  if (const char* e = std::getenv("PETDIFF_FUSE_DOWN1")) h->fuse_down1 = std::atoi(e) != 0;
   h->fuse_up = cfg->dtype != PETDIFF_DTYPE_F32;
   if (const char* e = std::getenv("PETDIFF_FUSE_UP")) h->fuse_up = h->fuse_up && std::atoi(e) != 0;
   const size_t need = h->spec.back().off + h->spec.back().size;
@@ -866,6 +882,7 @@ int petdiff_generate(petdiff_handle h, const float* x_T, const int32_t* tac, con
         io.skip_down0 = i > 0;
         io.fuse_next = i + 1 < n_steps;
         io.next_t = io.fuse_next ? t_seq[i + 1] : -1;
+        io.d1_ok = h->fuse_down1;
       }
       CHK(network(h, io, Bk, q));
     }

@@ -592,6 +592,120 @@ struct DmaPlan {
   }
 };
 
+// Fused down1 of the next reverse step, run by the final level's 4 waves on the tile's 4 samples:
+// relu(conv6(p0) + conv1(p0) + maps) -> s1 and MaxPool -> p1 (networks.py:589-711), as the
+// standalone conv_kernel<down1> computes it -- the same bf16 operands and fp32 MFMA accumulation
+// order (chunk of 32 channels, tap, k-group of 16), so the results are bitwise equal.  Wave w owns
+// output channels [64 w, 64 w + 64) (N-tile w of down1's packed weights); its B fragments stream
+// from L2 through a 4-deep register ring, its A fragments come from the p0 rows in LDS.
+// Fused down1 (FinalArgs::d1_w) tile in the final level's LDS, after the down0 map rows [48][128] f32:
+// A = p0 rows of the tile's samples [4 x 24 + zero row][128] bf16 (272-B rows: a 16-lane group's
+// ds_read_b128 covers all 64 banks), then the level-1 map rows [24][256] f32 (time + label + biases).
+constexpr int kD1Ldb = 272, kD1A = 48 * 128 * 4, kD1Rows = 4 * 24, kD1M = kD1A + (kD1Rows + 1) * kD1Ldb;
+
+// Measured (profiles/r02/ab/fused_down1): up2 40 -> 55.6-58.4 us with the fusion against 14.5 us
+// for the standalone down1 launch, 1.3 % slower end to end; diagnostic builds without the s1 / p1
+// stores (53.6 us) or without the MFMAs (53.6 us) show the cost is the B stream and staging, not the
+// arithmetic.  Neither the chunk rotation nor a 6-deep B ring moved it.  PETDIFF_FUSE_DOWN1 is off.
+#ifndef FD1_ROT
+#define FD1_ROT 0
+#endif
+#ifndef FD1_RING
+#define FD1_RING 6
+#endif
+// diagnostic builds: 1 = no s1 / p1 stores (one guarded store keeps the results live), 2 = no MFMAs
+#ifndef FD1_DIAG
+#define FD1_DIAG 0
+#endif
+template <typename FA>
+__device__ __forceinline__ void fused_down1(const FA& f, char* smem, int m0, int nb, int w, int lane) {
+  constexpr int NTD = 64, ROWBD = 64, BBYTES = 6 * NTD * ROWBD, TILE = 4 * BBYTES;   // 4 chunks of 32 ch
+  const int lr = lane & 31, h = lane >> 5;
+  int aoff[6][3];
+#pragma unroll
+  for (int j = 0; j < 6; ++j)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int r = i * 32 + lr, sm = r / 24, l = r - 24 * sm, p = l + j - 2;
+      const int row = (p >= 0 && p < 24) ? sm * 24 + p : kD1Rows;
+      aoff[j][i] = kD1A + row * kD1Ldb + h * 16;
+    }
+  const char* wb = reinterpret_cast<const char*>(f.d1_w) + (size_t)w * TILE;
+  int boff[2];
+#pragma unroll
+  for (int jn = 0; jn < 2; ++jn) {
+    const int n = jn * 32 + lr;
+    boff[jn] = n * ROWBD + ((h ^ ((n >> 2) & 3)) << 4);
+  }
+  // FD1_ROT: the chunk order starts at chunk (blockIdx / 8) mod 4, so the 32 workgroups of an XCD
+  // do not all stream the same weight lines at once (changes the fp32 accumulation order: not
+  // bitwise equal to the standalone launch)
+  const int rot = FD1_ROT ? (int)((blockIdx.x >> 3) & 3) : 0;
+  constexpr int RING = FD1_RING;
+  bf16x8 bq[RING][2][2];
+  auto ldb = [&](int it, bf16x8 (&dst)[2][2]) {
+    const char* base = wb + (((it / 6) + rot) & 3) * BBYTES + (it % 6) * NTD * ROWBD;
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn) dst[g][jn] = *reinterpret_cast<const bf16x8*>(base + (boff[jn] ^ (g << 5)));
+  };
+  f32x16 acc[3][2];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][jn][e] = 0.f;
+#pragma unroll
+  for (int it = 0; it < RING - 1; ++it) ldb(it, bq[it]);
+#pragma unroll
+  for (int it = 0; it < 24; ++it) {              // (chunk kc, tap j) = ((it / 6 + rot) mod 4, it % 6)
+    if (it + RING - 1 < 24) ldb(it + RING - 1, bq[(it + RING - 1) % RING]);
+    const int kc = ((it / 6) + rot) & 3, j = it % 6;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      bf16x8 av[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) av[i] = *reinterpret_cast<const bf16x8*>(smem + aoff[j][i] + kc * 64 + g * 32);
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int jn = 0; jn < 2; ++jn) {
+          if constexpr (FD1_DIAG == 2) acc[i][jn][0] += (float)av[i][0] * (float)bq[it % RING][g][jn][0];
+          else acc[i][jn] = mfma32(av[i], bq[it % RING][g][jn], acc[i][jn]);
+        }
+    }
+  }
+  // epilogue from registers: accumulator rows (e, e + 1) are positions (l, l + 1) of one sample
+  const float* md = reinterpret_cast<const float*>(smem + kD1M);
+  bf16* s1 = reinterpret_cast<bf16*>(f.d1_s1);
+  bf16* p1 = reinterpret_cast<bf16*>(f.d1_p1);
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int jn = 0; jn < 2; ++jn) {
+      const int n = w * NTD + jn * 32 + lr;
+#pragma unroll
+      for (int e = 0; e < 16; e += 2) {
+        const int r = i * 32 + 8 * (e >> 2) + 4 * h + (e & 3);
+        const int sm = r / 24, l = r - 24 * sm;
+        if (sm < nb) {
+          const float v0 = fmaxf(acc[i][jn][e] + md[l * 256 + n], 0.f);
+          const float v1 = fmaxf(acc[i][jn][e + 1] + md[(l + 1) * 256 + n], 0.f);
+          const size_t row = (size_t)(m0 + sm) * 24 + l;
+          if constexpr (FD1_DIAG == 1) {
+            if (v0 == 12345.f && v1 == 54321.f) s1[row * 256 + n] = (bf16)v0;
+            continue;
+          }
+          s1[row * 256 + n] = (bf16)v0;
+          s1[(row + 1) * 256 + n] = (bf16)v1;
+          p1[((size_t)(m0 + sm) * 12 + (l >> 1)) * 256 + n] = (bf16)fmaxf(v0, v1);
+        }
+      }
+    }
+}
+
 template <typename T> struct Vec8;
 #ifndef CONV_NT_STORE
 // activation stores: 1 non-temporal hint (A/B vs plain: +3.4% end to end, scripts/ab_bench.sh);
@@ -670,7 +784,7 @@ __device__ __forceinline__ void store_act(T* base, size_t row, int C, int n, con
 template <typename T, int XS = 0>
 __device__ __forceinline__ void down0_positions(const Down0Args& a, const float* xs, const float* mp, bool fast,
                                                 int b0, int nb, const f32x4 (&wr)[12][2], int n0, int pos0,
-                                                int pstride) {
+                                                int pstride, char* p0l = nullptr) {
   for (int pos = pos0; pos < nb * 24; pos += pstride) {
     const int bl = pos / 24, lp = pos - bl * 24, b = b0 + bl;
     const int l0 = 2 * lp;
@@ -720,6 +834,14 @@ __device__ __forceinline__ void down0_positions(const Down0Args& a, const float*
     for (int q = 0; q < 8; ++q) pv[q] = fmaxf(v[0][q], v[1][q]);
     if constexpr (!(FIN_EXP & 2)) store_act<T, XS>(reinterpret_cast<T*>(a.p0), (size_t)b * 24 + lp, 128, n0, pv);
     else if (pv[0] == 12345.f) reinterpret_cast<T*>(a.p0)[0] = (T)0.f;
+    if constexpr (sizeof(T) == 2 && XS == 0) {
+      if (p0l) {   // fused down1: the same bf16 row, LDS row bl * 24 + lp (kD1Ldb bytes per row)
+        typename Frag<T>::type o;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) o[q] = (T)pv[q];
+        *reinterpret_cast<typename Frag<T>::type*>(p0l + (bl * 24 + lp) * kD1Ldb + n0 * 2) = o;
+      }
+    }
   }
 }
 
@@ -1913,8 +2035,32 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
 #pragma unroll
         for (int k = 0; k < 6; ++k) reinterpret_cast<f32x4*>(mp)[tid + kThreads * k] = mv[k];
       }
+      // fused down1 (one condition, bf16): level-1 map rows loaded now, written to LDS after down0
+      constexpr bool D1 = std::is_same<T, bf16>::value && XS == 0 && G::FIN_MAPS;
+      const bool fuse_d1 = D1 && f.d1_w != nullptr && fast;
+      static_assert(!D1 || kD1M + 24 * 256 * 4 <= G::MT * G::FIN_LD * 4, "fused down1 tiles fit the dead C tile");
+      static_assert(!D1 || G::MT / L == 4, "fused down1: 4 samples per tile");
+      f32x4 m1v[6];
+      if (fuse_d1) {
+        const f32x4* tm1 = reinterpret_cast<const f32x4*>(f.d1_tmap + (size_t)nd.t_uniform * 24 * 256);
+        const f32x4* cm1 = reinterpret_cast<const f32x4*>(f.d1_cmap);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) m1v[k] = tm1[tid + kThreads * k] + cm1[tid + kThreads * k];
+        // zero row + the rows of absent samples (their outputs are not stored; keep them finite)
+        for (int q = tid; q < (kD1Rows + 1 - nb_next * 24) * (kD1Ldb / 16); q += kThreads)
+          *reinterpret_cast<uint4*>(smem + kD1A + nb_next * 24 * kD1Ldb + q * 16) = make_uint4(0, 0, 0, 0);
+      }
       __syncthreads();
-      if constexpr (!(FIN_EXP & 1)) down0_positions<T, XS>(nd, xst, mp, fast, m0, nb_next, wr, n0_next, tid >> 4, kThreads / 16);
+      if constexpr (!(FIN_EXP & 1)) down0_positions<T, XS>(nd, xst, mp, fast, m0, nb_next, wr, n0_next, tid >> 4, kThreads / 16,
+                                                           fuse_d1 ? smem + kD1A : nullptr);
+      if constexpr (D1) {
+        if (fuse_d1) {
+#pragma unroll
+          for (int k = 0; k < 6; ++k) reinterpret_cast<f32x4*>(smem + kD1M)[tid + kThreads * k] = m1v[k];
+          __syncthreads();                             // p0 rows and level-1 maps in LDS
+          fused_down1(f, smem, m0, nb_next, wv, lane);
+        }
+      }
 #if CONV_EXP_MODE & 128
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();

@@ -371,6 +371,28 @@ def test_fused_next_step_down0_bitwise(conds, dtype, monkeypatch):
     fused.close()
 
 
+def test_fused_next_step_down1_bitwise(conds, monkeypatch):
+    """PETDIFF_FUSE_DOWN1=1 also runs step i+1's down1 (Conv1D 128 -> 256 + MaxPool) inside step i's
+    final epilogue, on the tile's own p0 rows (bf16, one condition; measured slower, so off by
+    default).  Same operands and fp32 MFMA accumulation order as the standalone conv_kernel<down1>:
+    bit-identical samples, ragged batch (an incomplete last tile), graph and eager."""
+    rng = np.random.default_rng(25)
+    B = 37
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    monkeypatch.setenv('PETDIFF_FUSE_DOWN1', '0')
+    plain = make_model('bfloat16')
+    plain._ensure_handle()
+    monkeypatch.setenv('PETDIFF_FUSE_DOWN1', '1')
+    fused = make_model('bfloat16')
+    fused._ensure_handle()
+    for g in (True, False):
+        a = plain.ddpm_loop(x, conds[:1], num_timesteps=25, seed=4, use_graph=g)
+        b = fused.ddpm_loop(x, conds[:1], num_timesteps=25, seed=4, use_graph=g)
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    plain.close()
+    fused.close()
+
+
 def test_split_streams_bitwise(conds, monkeypatch):
     """PETDIFF_SPLIT=2 runs the batch as two sample ranges, each its own graph on its own
     stream: identical samples to the single-graph run (counter-based noise, per-sample math)."""
