@@ -603,10 +603,11 @@ struct DmaPlan {
 // ds_read_b128 covers all 64 banks), then the level-1 map rows [24][256] f32 (time + label + biases).
 constexpr int kD1Ldb = 272, kD1A = 48 * 128 * 4, kD1Rows = 4 * 24, kD1M = kD1A + (kD1Rows + 1) * kD1Ldb;
 
-// Measured (profiles/r02/ab/fused_down1): up2 40 -> 55.6-58.4 us with the fusion against 14.5 us
-// for the standalone down1 launch, 1.3 % slower end to end; diagnostic builds without the s1 / p1
-// stores (53.6 us) or without the MFMAs (53.6 us) show the cost is the B stream and staging, not the
-// arithmetic.  Neither the chunk rotation nor a 6-deep B ring moved it.  PETDIFF_FUSE_DOWN1 is off.
+// Measured (profiles/r02/ab/fused_down1): the first version cost 15-18 us inside up2 against 14.5 us
+// for the standalone down1 launch (1.3 % slower end to end): the compiler had sunk every B load to
+// just before its MFMAs (vmcnt(1..3) waits).  With sched_barriers holding the B ring RING - 1
+// iterations ahead, A reads one step ahead, and no global p0 copy: up2 54.8 us and +0.3..0.8 % end
+// to end in three A/B calls; on by default (PETDIFF_FUSE_DOWN1=0 restores the standalone launch).
 #ifndef FD1_ROT
 #define FD1_ROT 0
 #endif
@@ -659,23 +660,32 @@ __device__ __forceinline__ void fused_down1(const FA& f, char* smem, int m0, int
       for (int e = 0; e < 16; ++e) acc[i][jn][e] = 0.f;
 #pragma unroll
   for (int it = 0; it < RING - 1; ++it) ldb(it, bq[it]);
+  // A fragments of step st = 2 it + g (chunk kc, tap j, k-group g), read one step ahead
+  auto lda = [&](int st, bf16x8 (&dst)[3]) {
+    const int it = st >> 1, g = st & 1, kc = ((it / 6) + rot) & 3, j = it % 6;
 #pragma unroll
-  for (int it = 0; it < 24; ++it) {              // (chunk kc, tap j) = ((it / 6 + rot) mod 4, it % 6)
-    if (it + RING - 1 < 24) ldb(it + RING - 1, bq[(it + RING - 1) % RING]);
-    const int kc = ((it / 6) + rot) & 3, j = it % 6;
+    for (int i = 0; i < 3; ++i) dst[i] = *reinterpret_cast<const bf16x8*>(smem + aoff[j][i] + kc * 64 + g * 32);
+  };
+  bf16x8 av[2][3];
+  lda(0, av[0]);
+  // the scheduler would sink each B load to just before its MFMAs (vmcnt(1..3) waits, a
+  // latency-bound stream) and each A read likewise; the barriers keep the B ring RING - 1
+  // iterations and the A reads one step ahead
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      bf16x8 av[3];
+  for (int st = 0; st < 48; ++st) {              // (chunk kc, tap j) = ((it / 6 + rot) mod 4, it % 6)
+    const int it = st >> 1, g = st & 1;
+    if (g == 0 && it + RING - 1 < 24) ldb(it + RING - 1, bq[(it + RING - 1) % RING]);
+    if (st + 1 < 48) lda(st + 1, av[(st + 1) & 1]);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < 3; ++i) av[i] = *reinterpret_cast<const bf16x8*>(smem + aoff[j][i] + kc * 64 + g * 32);
+    for (int i = 0; i < 3; ++i)
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int jn = 0; jn < 2; ++jn) {
-          if constexpr (FD1_DIAG == 2) acc[i][jn][0] += (float)av[i][0] * (float)bq[it % RING][g][jn][0];
-          else acc[i][jn] = mfma32(av[i], bq[it % RING][g][jn], acc[i][jn]);
-        }
-    }
+      for (int jn = 0; jn < 2; ++jn) {
+        if constexpr (FD1_DIAG == 2) acc[i][jn][0] += (float)av[st & 1][i][0] * (float)bq[it % RING][g][jn][0];
+        else acc[i][jn] = mfma32(av[st & 1][i], bq[it % RING][g][jn], acc[i][jn]);
+      }
+    __builtin_amdgcn_sched_barrier(0);
   }
   // epilogue from registers: accumulator rows (e, e + 1) are positions (l, l + 1) of one sample
   const float* md = reinterpret_cast<const float*>(smem + kD1M);
@@ -832,7 +842,8 @@ __device__ __forceinline__ void down0_positions(const Down0Args& a, const float*
     float pv[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) pv[q] = fmaxf(v[0][q], v[1][q]);
-    if constexpr (!(FIN_EXP & 2)) store_act<T, XS>(reinterpret_cast<T*>(a.p0), (size_t)b * 24 + lp, 128, n0, pv);
+    // p0 feeds only down1: with the fused down1 (p0l) it stays in LDS, no global copy
+    if constexpr (!(FIN_EXP & 2)) { if (!p0l) store_act<T, XS>(reinterpret_cast<T*>(a.p0), (size_t)b * 24 + lp, 128, n0, pv); }
     else if (pv[0] == 12345.f) reinterpret_cast<T*>(a.p0)[0] = (T)0.f;
     if constexpr (sizeof(T) == 2 && XS == 0) {
       if (p0l) {   // fused down1: the same bf16 row, LDS row bl * 24 + lp (kD1Ldb bytes per row)

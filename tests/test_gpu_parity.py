@@ -373,8 +373,8 @@ def test_fused_next_step_down0_bitwise(conds, dtype, monkeypatch):
 
 def test_fused_next_step_down1_bitwise(conds, monkeypatch):
     """PETDIFF_FUSE_DOWN1=1 also runs step i+1's down1 (Conv1D 128 -> 256 + MaxPool) inside step i's
-    final epilogue, on the tile's own p0 rows (bf16, one condition; measured slower, so off by
-    default).  Same operands and fp32 MFMA accumulation order as the standalone conv_kernel<down1>:
+    final epilogue, on the tile's own p0 rows (bf16, one condition; on by default,
+    PETDIFF_FUSE_DOWN1=0 keeps the standalone launch).  Same operands and fp32 MFMA accumulation order as the standalone conv_kernel<down1>:
     bit-identical samples, ragged batch (an incomplete last tile), graph and eager."""
     rng = np.random.default_rng(25)
     B = 37
