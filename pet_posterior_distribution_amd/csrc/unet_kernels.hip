@@ -618,6 +618,12 @@ constexpr int kD1Ldb = 272, kD1A = 48 * 128 * 4, kD1Rows = 4 * 24, kD1M = kD1A +
 #ifndef FD1_DIAG
 #define FD1_DIAG 0
 #endif
+// s1 rows staged in LDS for 16-B stores (0: 2-B stores from registers).  Measured: staged 4753-4763
+// vs direct 4773-4777 samples/s (profiles/r02/ab/fused_down1/v6_stage): the extra barriers cost more
+// than the wider stores save.  Off.
+#ifndef FD1_STAGE
+#define FD1_STAGE 0
+#endif
 template <typename FA>
 __device__ __forceinline__ void fused_down1(const FA& f, char* smem, int m0, int nb, int w, int lane) {
   constexpr int NTD = 64, ROWBD = 64, BBYTES = 6 * NTD * ROWBD, TILE = 4 * BBYTES;   // 4 chunks of 32 ch
@@ -687,10 +693,15 @@ __device__ __forceinline__ void fused_down1(const FA& f, char* smem, int m0, int
       }
     __builtin_amdgcn_sched_barrier(0);
   }
-  // epilogue from registers: accumulator rows (e, e + 1) are positions (l, l + 1) of one sample
+  // epilogue: accumulator rows (e, e + 1) are positions (l, l + 1) of one sample.  The pooled p1
+  // goes out from registers (2-B stores); the s1 rows (FD1_STAGE) are staged as bf16 in this wave's
+  // [96][64] slice of the dead down0-map / A-tile region and leave as 16-B stores of 8 channels
   const float* md = reinterpret_cast<const float*>(smem + kD1M);
   bf16* s1 = reinterpret_cast<bf16*>(f.d1_s1);
   bf16* p1 = reinterpret_cast<bf16*>(f.d1_p1);
+  bf16* stg = reinterpret_cast<bf16*>(smem) + w * 96 * NTD;      // 12 KB per wave, below kD1M
+  static_assert(4 * 96 * NTD * 2 <= kD1M, "s1 staging stays below the level-1 map rows");
+  if (FD1_STAGE) __syncthreads();                // every wave is done with the A tile
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -700,20 +711,38 @@ __device__ __forceinline__ void fused_down1(const FA& f, char* smem, int m0, int
       for (int e = 0; e < 16; e += 2) {
         const int r = i * 32 + 8 * (e >> 2) + 4 * h + (e & 3);
         const int sm = r / 24, l = r - 24 * sm;
+        const float v0 = fmaxf(acc[i][jn][e] + md[l * 256 + n], 0.f);
+        const float v1 = fmaxf(acc[i][jn][e + 1] + md[(l + 1) * 256 + n], 0.f);
+        if (FD1_STAGE) {
+          stg[r * NTD + jn * 32 + lr] = (bf16)v0;
+          stg[(r + 1) * NTD + jn * 32 + lr] = (bf16)v1;
+        }
         if (sm < nb) {
-          const float v0 = fmaxf(acc[i][jn][e] + md[l * 256 + n], 0.f);
-          const float v1 = fmaxf(acc[i][jn][e + 1] + md[(l + 1) * 256 + n], 0.f);
           const size_t row = (size_t)(m0 + sm) * 24 + l;
           if constexpr (FD1_DIAG == 1) {
             if (v0 == 12345.f && v1 == 54321.f) s1[row * 256 + n] = (bf16)v0;
             continue;
           }
-          s1[row * 256 + n] = (bf16)v0;
-          s1[(row + 1) * 256 + n] = (bf16)v1;
+          if (!FD1_STAGE) {
+            s1[row * 256 + n] = (bf16)v0;
+            s1[(row + 1) * 256 + n] = (bf16)v1;
+          }
           p1[((size_t)(m0 + sm) * 12 + (l >> 1)) * 256 + n] = (bf16)fmaxf(v0, v1);
         }
       }
     }
+  if (FD1_STAGE && FD1_DIAG != 1) {
+    __syncthreads();                             // (the staging slices are per wave; one barrier)
+#pragma unroll
+    for (int q = 0; q < 12; ++q) {               // 96 rows x 8 pieces of 16 B per wave
+      const int pc = q * 64 + lane, r = pc >> 3, c8 = (pc & 7) * 8;
+      const int sm = r / 24, l = r - 24 * sm;
+      if (sm < nb) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(stg + r * NTD + c8);
+        *reinterpret_cast<bf16x8*>(s1 + ((size_t)(m0 + sm) * 24 + l) * 256 + w * NTD + c8) = v;
+      }
+    }
+  }
 }
 
 template <typename T> struct Vec8;
