@@ -624,9 +624,31 @@ constexpr int kD1Ldb = 272, kD1A = 48 * 128 * 4, kD1Rows = 4 * 24, kD1M = kD1A +
 #ifndef FD1_STAGE
 #define FD1_STAGE 0
 #endif
+// FD1_EARLY: the first RING - 1 iterations' B fragments are loaded before the fused down0 runs, so
+// their latency hides behind it (the ring lives in registers across down0).  Measured neutral
+// (4901 / 4880 vs 4904 / 4892 samples/s, profiles/r02/ab/fused_down1/v7_early): off
+#ifndef FD1_EARLY
+#define FD1_EARLY 0
+#endif
+// B fragments of iteration it (chunk it / 6 rotated by rot, tap it % 6), both k-groups and N-halves
 template <typename FA>
-__device__ __forceinline__ void fused_down1(const FA& f, char* smem, int m0, int nb, int w, int lane) {
-  constexpr int NTD = 64, ROWBD = 64, BBYTES = 6 * NTD * ROWBD, TILE = 4 * BBYTES;   // 4 chunks of 32 ch
+__device__ __forceinline__ void fd1_ldb(const FA& f, int w, int lane, int it, int rot, bf16x8 (&dst)[2][2]) {
+  constexpr int NTD = 64, ROWBD = 64, BBYTES = 6 * NTD * ROWBD, TILE = 4 * BBYTES;
+  const int lr = lane & 31, h = lane >> 5;
+  const char* base = reinterpret_cast<const char*>(f.d1_w) + (size_t)w * TILE + (((it / 6) + rot) & 3) * BBYTES +
+                     (it % 6) * NTD * ROWBD;
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int jn = 0; jn < 2; ++jn) {
+      const int n = jn * 32 + lr;
+      dst[g][jn] = *reinterpret_cast<const bf16x8*>(base + ((n * ROWBD + ((h ^ ((n >> 2) & 3)) << 4)) ^ (g << 5)));
+    }
+}
+template <typename FA>
+__device__ __forceinline__ void fused_down1(const FA& f, char* smem, int m0, int nb, int w, int lane,
+                                            bf16x8 (&bq)[FD1_RING][2][2]) {
+  constexpr int NTD = 64;   // output channels per wave (down1 N-tile)
   const int lr = lane & 31, h = lane >> 5;
   int aoff[6][3];
 #pragma unroll
@@ -637,26 +659,12 @@ __device__ __forceinline__ void fused_down1(const FA& f, char* smem, int m0, int
       const int row = (p >= 0 && p < 24) ? sm * 24 + p : kD1Rows;
       aoff[j][i] = kD1A + row * kD1Ldb + h * 16;
     }
-  const char* wb = reinterpret_cast<const char*>(f.d1_w) + (size_t)w * TILE;
-  int boff[2];
-#pragma unroll
-  for (int jn = 0; jn < 2; ++jn) {
-    const int n = jn * 32 + lr;
-    boff[jn] = n * ROWBD + ((h ^ ((n >> 2) & 3)) << 4);
-  }
   // FD1_ROT: the chunk order starts at chunk (blockIdx / 8) mod 4, so the 32 workgroups of an XCD
   // do not all stream the same weight lines at once (changes the fp32 accumulation order: not
   // bitwise equal to the standalone launch)
   const int rot = FD1_ROT ? (int)((blockIdx.x >> 3) & 3) : 0;
   constexpr int RING = FD1_RING;
-  bf16x8 bq[RING][2][2];
-  auto ldb = [&](int it, bf16x8 (&dst)[2][2]) {
-    const char* base = wb + (((it / 6) + rot) & 3) * BBYTES + (it % 6) * NTD * ROWBD;
-#pragma unroll
-    for (int g = 0; g < 2; ++g)
-#pragma unroll
-      for (int jn = 0; jn < 2; ++jn) dst[g][jn] = *reinterpret_cast<const bf16x8*>(base + (boff[jn] ^ (g << 5)));
-  };
+  auto ldb = [&](int it, bf16x8 (&dst)[2][2]) { fd1_ldb(f, w, lane, it, rot, dst); };
   f32x16 acc[3][2];
 #pragma unroll
   for (int i = 0; i < 3; ++i)
@@ -664,8 +672,10 @@ __device__ __forceinline__ void fused_down1(const FA& f, char* smem, int m0, int
     for (int jn = 0; jn < 2; ++jn)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][jn][e] = 0.f;
+  if (!FD1_EARLY || FD1_ROT) {
 #pragma unroll
-  for (int it = 0; it < RING - 1; ++it) ldb(it, bq[it]);
+    for (int it = 0; it < RING - 1; ++it) ldb(it, bq[it]);
+  }
   // A fragments of step st = 2 it + g (chunk kc, tap j, k-group g), read one step ahead
   auto lda = [&](int st, bf16x8 (&dst)[3]) {
     const int it = st >> 1, g = st & 1, kc = ((it / 6) + rot) & 3, j = it % 6;
@@ -2081,7 +2091,12 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
       static_assert(!D1 || kD1M + 24 * 256 * 4 <= G::MT * G::FIN_LD * 4, "fused down1 tiles fit the dead C tile");
       static_assert(!D1 || G::MT / L == 4, "fused down1: 4 samples per tile");
       f32x4 m1v[6];
+      bf16x8 bqd[FD1_RING][2][2];
       if (fuse_d1) {
+        if (FD1_EARLY && !FD1_ROT) {
+#pragma unroll
+          for (int it = 0; it < FD1_RING - 1; ++it) fd1_ldb(f, wv, lane, it, 0, bqd[it]);
+        }
         const f32x4* tm1 = reinterpret_cast<const f32x4*>(f.d1_tmap + (size_t)nd.t_uniform * 24 * 256);
         const f32x4* cm1 = reinterpret_cast<const f32x4*>(f.d1_cmap);
 #pragma unroll
@@ -2098,7 +2113,7 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
 #pragma unroll
           for (int k = 0; k < 6; ++k) reinterpret_cast<f32x4*>(smem + kD1M)[tid + kThreads * k] = m1v[k];
           __syncthreads();                             // p0 rows and level-1 maps in LDS
-          fused_down1(f, smem, m0, nb_next, wv, lane);
+          fused_down1(f, smem, m0, nb_next, wv, lane, bqd);
         }
       }
 #if CONV_EXP_MODE & 128
