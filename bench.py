@@ -6,11 +6,11 @@ iDDPM reverse (ImprovedDDPM.ddpm_loop, diffusion_model.py:670-715), n_posterior 
 1024 samples per GPU, bf16 network / fp32 p_sample, one synthetic test TAC per
 GPU, synthetic (identity-denoiser Glorot) weights of the shipped architecture.
 
-A bench "step" = one full generate() (1000 reverse steps) over the rank's 1024
-samples; the whole loop is one replayed hipGraph.  Weak scaling: every rank
-owns 1024 samples of its own TAC; value = all ranks' samples / max-over-ranks time.
-After the timed region the per-(TAC, ROI, param) Welford partials are
-all-gathered over RCCL (the only collective).
+A bench "step" = one whole posterior job through distributed.sample_posterior_sharded (the
+configs[3] driver): x_T, one full generate() (1000 reverse steps, one replayed hipGraph) over
+the rank's 1024 samples, the GPU Welford statistics and their all-gather over RCCL (the only
+collective).  Weak scaling: every rank owns 1024 samples of its own TAC
+(TAC-major shards); value = all ranks' samples / max-over-ranks time.
 
 Launch: python bench.py --gpus N --steps K --warmup W  (N>1 via torch.distributed.run).
 """
@@ -176,19 +176,34 @@ def cpu_baseline(weights, cond, budget_s=15.0):
                       f'reverse steps ({dt:.1f} s), extrapolated to 1000 steps'}
 
 
-def load_pmc(fused_up=False):
+NO_PMC = {'traffic': None, 'mfma_busy': None, 'grbm': None, 'source': None}
+
+
+def load_pmc(fused_up=False, dtype='bfloat16'):
     """Per-launch PMC figures of the dominant kernel from the committed rocprofv3 summary
-    (profiles/pmc_traffic.json): HBM bytes (FETCH_SIZE x2 + WRITE_SIZE), SQ_VALU_MFMA_BUSY_CYCLES
-    and GRBM_GUI_ACTIVE; missing entries are None."""
-    pre = 'up0_fused' if fused_up else 'up0_block'
+    (profiles/pmc_traffic.json, written by scripts/pmc_summary.py --traffic): HBM bytes (FETCH_SIZE x2 +
+    WRITE_SIZE), SQ_VALU_MFMA_BUSY_CYCLES and GRBM_GUI_ACTIVE.  The entries are stamped with the
+    code-object hash of the U-Net kernels they were counted on (_lib.kernel_code_hash); when the
+    loaded library's kernels differ, the counters belong to another build and every field is None
+    (pmc_stale says so).  Missing entries are None."""
+    from pet_posterior_distribution_amd import _lib
+    pre = ('up0_fused' if fused_up else 'up0_block') + {'bfloat16': '', 'bf16x3': '_bf16x3',
+                                                      'float16': '_f16'}.get(dtype, '_none')
     p = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     try:
         with open(p) as f:
             d = json.load(f)
     except Exception:
         d = {}
-    return {k: d.get(pre + suf) for k, suf in (('traffic', '_bytes_per_launch'), ('mfma_busy', '_mfma_busy_cycles'),
-                                                ('grbm', '_grbm_gui_active'), ('source', '_source'))}
+    have, now = d.get(pre + '_code_hash'), _lib.kernel_code_hash()
+    out = dict(NO_PMC)
+    if have is not None and have == now:
+        out = {k: d.get(pre + suf) for k, suf in (('traffic', '_bytes_per_launch'), ('mfma_busy', '_mfma_busy_cycles'),
+                                                  ('grbm', '_grbm_gui_active'), ('source', '_source'))}
+    out['code_hash'] = now
+    out['stale'] = have != now
+    out['counted_on'] = have
+    return out
 
 
 def pmc_fields(pmc, avg_s):
@@ -207,7 +222,43 @@ def pmc_fields(pmc, avg_s):
         if pmc['grbm']:
             out['mfma_busy_vs_active'] = round(pmc['mfma_busy'] / (N_SIMD * pmc['grbm'] / 8), 4)
     out['pmc_source'] = pmc['source']
+    out['pmc_code_hash'] = pmc.get('code_hash')
+    out['pmc_stale'] = pmc.get('stale')
     return out
+
+
+def up0_roofline(layer_ms, bt, dtype, tflops_pipeline=None):
+    """`roofline` of the dominant kernel (up0's fused level; up0.block when unfused) from per-layer HIP-event
+    timing (ms, count) of one eager generate at bt samples per launch: algorithmic FLOP per launch / mean
+    launch time against the dtype's dense MFMA peak (fp16 dense = bf16 dense; bf16x3 runs 3 bf16 products
+    per fp32 product, so its peak is bf16 dense / 3; f32: the fp32 MFMA peak), plus the PMC fields of the
+    same kernel and dtype when the committed counters were taken on this build (load_pmc)."""
+    peak = {'float32': PEAK_F32_TFLOPS, 'bf16x3': PEAK_BF16_TFLOPS / 3}.get(dtype, PEAK_BF16_TFLOPS)
+    ms, cnt = layer_ms['up0.block']
+    avg_s = ms / max(cnt, 1) / 1e3
+    fused_up = layer_ms['up0.conv2'][1] == 0      # the k2 conv runs inside the block kernel
+    alg = UP0_BLOCK_FLOP_PER_SAMPLE + (UP0_CONV2_FLOP_PER_SAMPLE if fused_up else 0)
+    exe = UP0_FUSED_EXEC_FLOP_PER_SAMPLE if fused_up else UP0_BLOCK_EXEC_FLOP_PER_SAMPLE
+    ach = alg * bt / avg_s / 1e12
+    # the PMC passes are taken at B = 1024 (config 2), per dtype
+    pmc = load_pmc(fused_up, dtype) if bt == 1024 else dict(NO_PMC)
+    kname = ('conv_kernel<up0 fused> (UpSampling1D + k2 conv 1074->512 + ConvBlock 1024->512 k6+res, L=12)'
+             if fused_up else 'conv_kernel<up0.block> (L=12, 1024->512, k6+res)')
+    roof = {'bound': 'mfma', 'kernel': kname + (' [bf16x3: 3 bf16 MFMA products per fp32 product]'
+                                               if dtype == 'bf16x3' else ''),
+            'achieved': round(ach, 2), 'peak': round(peak, 2), 'unit': 'TFLOP/s', 'frac': round(ach / peak, 4),
+            'traffic': pmc['traffic'], 'avg_launch_us': round(avg_s * 1e6, 2),
+            'executed_tflops': round((3 if dtype == 'bf16x3' else 1) * exe * bt / avg_s / 1e12, 2)}
+    if tflops_pipeline is not None:
+        roof['pipeline_tflops'] = round(tflops_pipeline, 2)
+        roof['pipeline_frac'] = round(tflops_pipeline / peak, 4)
+    roof.update(pmc_fields(pmc, avg_s))
+    return roof
+
+
+def layer_us(layer_ms):
+    return {k: round(v[0] / max(v[1], 1) * 1e3, 2) for k, v in layer_ms.items()}
+
 
 
 # MH cost per element update (one ROI's SRTM2 + 54 truncated-normal terms), counted
@@ -442,11 +493,18 @@ def bf16x3_rate(cond, B, n_rev, dev):
     el = time.perf_counter() - t0
     tf = FLOP_PER_SAMPLE_STEP * n_rev * B / el / 1e12
     te = 3 * EXEC_MFMA_FLOP_PER_SAMPLE_STEP_FUSED * n_rev * B / el / 1e12
+    # the dominant kernel of THIS network: per-layer HIP events over one eager generate on the launch stream
+    m.set_kernel_timing(True)
+    m.ddpm_loop(x, cond[None], num_timesteps=n_rev, seed=2, use_graph=False)
+    lm = m.get_kernel_timing()
+    m.set_kernel_timing(False)
     m.close()
     return {'value': round(B / el, 2), 'unit': 'samples/s', 'dtype': 'bf16x3 (fp32-class)', 'n_posterior': B,
             'reverse_steps': n_rev, 'ms_per_generate': round(el * 1e3, 2),
             'pipeline_tflops': round(tf, 2), 'frac_vs_f32_peak': round(tf / PEAK_F32_TFLOPS, 4),
+            'pipeline_frac_vs_bf16x3_peak': round(tf / (PEAK_BF16_TFLOPS / 3), 4),
             'executed_bf16_tflops': round(te, 2), 'executed_frac': round(te / PEAK_BF16_TFLOPS, 4),
+            'roofline': up0_roofline(lm, B, 'bf16x3'), 'layer_us': layer_us(lm),
             'finite': bool(torch.isfinite(out).all())}
 
 
@@ -557,22 +615,28 @@ def main():
     n_tac = args.tacs
     if n_tac < 1 or B % n_tac:
         raise SystemExit('--batch must be a multiple of --tacs')
-    # the rank's synthetic test TACs (global TAC index rank * n_tac + k), samples TAC-major
-    cond = np.stack([make_condition(seed=rank * n_tac + k) for k in range(n_tac)])
-    tac = torch.arange(n_tac, device=dev, dtype=torch.int32).repeat_interleave(B // n_tac)
-    g = torch.Generator(device=dev)
-    g.manual_seed(1000 + rank)
-    x_T = torch.randn((B, 48, 2), generator=g, device=dev, dtype=torch.float32)
+    # BASELINE configs[3]'s product path (distributed.sample_posterior_sharded, tests/test_gpu_sharded.py):
+    # world * n_tac synthetic test TACs (TAC k = make_condition(seed=k)) x B / n_tac posterior samples each,
+    # sharded TAC-major, so rank r owns TACs r * n_tac .. r * n_tac + n_tac - 1 and global samples
+    # r * B .. r * B + B - 1; x_T and z from the counter-based Philox stream keyed by the global sample index.
+    # One bench step = one whole job: x_T, the 1000-step generate (one replayed hipGraph per launch of
+    # <= PETDIFF_MAX_BATCH samples), the GPU Welford statistics and their all-gather + merge.
+    from pet_posterior_distribution_amd.distributed import TacTable, sample_posterior_sharded
+    n_per = B // n_tac
+    table = TacTable(world * n_tac, lambda k: make_condition(seed=k))
+    cond = table.rows(range(rank * n_tac, rank * n_tac + n_tac))          # this rank's TACs (built once)
+    coll = coll_device(dev) if world > 1 else None
     n_rev = args.reverse_steps
     offset = rank * B
+    ag = {'ms': 0.0}
 
     def one():
-        return model.ddpm_loop(x_T, cond, num_timesteps=n_rev, seed=2, sample_offset=offset,
-                               tac=tac if n_tac > 1 else None)
+        return sample_posterior_sharded(model, table, n_per, seed=2, x_T_seed=1, num_timesteps=n_rev,
+                                        return_samples=True, coll_device=coll)
 
     long_run = B > chunk                      # e.g. --config4: about a minute per step; say so on stderr
     for i in range(args.warmup):
-        out = one()
+        res = one()
         if long_run:
             torch.cuda.synchronize()
             print(f'[bench] warmup {i + 1}/{args.warmup} done', file=sys.stderr, flush=True)
@@ -582,9 +646,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        out = one()
-        if long_run:                          # the sync is inside the timed region only for these runs,
-            torch.cuda.synchronize()          # where one step is ~1 minute of GPU work
+        res = one()
+        if long_run:
             print(f'[bench] step {i + 1}/{args.steps} done', file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if world > 1:
@@ -593,22 +656,19 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         elapsed = max_over_ranks(elapsed, dev)
-
-    # posterior summary: per-rank Welford partials, RCCL all-gather
-    st = model.posterior_stats(out, tac=tac if n_tac > 1 else None, n_tac=n_tac)   # (n_tac, 48, 2, 3) fp64
-    st_t = torch.as_tensor(st, device=coll_device(dev) if world > 1 else dev)
-    ag_ms = 0.0
-    if world > 1:
-        gathered = [torch.empty_like(st_t) for _ in range(world)]
+    _, allst, (lo, hi, out) = res
+    assert (lo, hi) == (offset, offset + B)
+    if world > 1:                              # the all-gather alone, timed once after the loop
+        from pet_posterior_distribution_amd.distributed import allgather_stats
         torch.cuda.synchronize()
         ta = time.perf_counter()
-        dist.all_gather(gathered, st_t)
+        allgather_stats(allst, device=coll)
         torch.cuda.synchronize()
-        ag_ms = (time.perf_counter() - ta) * 1e3
-        allst = torch.cat(gathered).cpu().numpy()
-    else:
-        allst = st
+        ag['ms'] = (time.perf_counter() - ta) * 1e3
+    ag_ms = ag['ms']
     finite = bool(torch.isfinite(out).all())
+    x_T = model.philox_normal(min(B, chunk), seed=1, sample_offset=offset)
+    tac = torch.arange(n_tac, device=dev, dtype=torch.int32).repeat_interleave(n_per)
 
     # per-layer kernel timing (HIP events on the launch stream, one eager generate)
     layer_ms = None
@@ -624,27 +684,7 @@ def main():
         samples = world * B * args.steps
         value = samples / elapsed
         tflops_pipeline = FLOP_PER_SAMPLE_STEP * n_rev * samples / elapsed / 1e12
-        # fp16 dense = bf16 dense; bf16x3 runs 3 bf16 MFMA products per fp32 product
-        peak = {'float32': PEAK_F32_TFLOPS, 'bf16x3': PEAK_BF16_TFLOPS / 3}.get(args.dtype, PEAK_BF16_TFLOPS)
-        roof = None
-        if layer_ms is not None:
-            ms, cnt = layer_ms['up0.block']
-            avg_s = ms / max(cnt, 1) / 1e3
-            fused_up = layer_ms['up0.conv2'][1] == 0      # the k2 conv runs inside the block kernel
-            alg = UP0_BLOCK_FLOP_PER_SAMPLE + (UP0_CONV2_FLOP_PER_SAMPLE if fused_up else 0)
-            exe = UP0_FUSED_EXEC_FLOP_PER_SAMPLE if fused_up else UP0_BLOCK_EXEC_FLOP_PER_SAMPLE
-            ach = alg * bt / avg_s / 1e12
-            # the PMC passes are taken at B = 1024, bf16 (config 2); other launch sizes / dtypes get none
-            pmc = load_pmc(fused_up) if (bt == 1024 and args.dtype == 'bfloat16') else {'traffic': None, 'mfma_busy': None, 'grbm': None, 'source': None}
-            kname = ('conv_kernel<up0 fused> (UpSampling1D + k2 conv 1074->512 + ConvBlock 1024->512 k6+res, L=12)'
-                     if fused_up else 'conv_kernel<up0.block> (L=12, 1024->512, k6+res)')
-            roof = {'bound': 'mfma', 'kernel': kname,
-                    'achieved': round(ach, 2), 'peak': peak, 'unit': 'TFLOP/s', 'frac': round(ach / peak, 4),
-                    'traffic': pmc['traffic'], 'avg_launch_us': round(avg_s * 1e6, 2),
-                    'executed_tflops': round((3 if args.dtype == 'bf16x3' else 1) * exe * bt / avg_s / 1e12, 2),
-                    'pipeline_tflops': round(tflops_pipeline, 2),
-                    'pipeline_frac': round(tflops_pipeline / peak, 4)}
-            roof.update(pmc_fields(pmc, avg_s))
+        roof = up0_roofline(layer_ms, bt, args.dtype, tflops_pipeline) if layer_ms is not None else None
         line = {
             'metric': 'posterior samples/sec (48-ROI TAC, 1000-step reverse) at 1/2/4/8 MI355X',
             'value': round(value, 2), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
@@ -655,14 +695,15 @@ def main():
             'config': {'workload': 'iDDPM reverse process, f128/d4 1-D conditional U-Net, 48-ROI x 2 params',
                        'n_posterior_per_gpu': B, 'reverse_steps': n_rev, 'global_batch': world * B,
                        'tacs': world * n_tac, 'samples_per_launch': min(B, chunk),
-                       'parallelism': f'dp{world} (sample shards, RCCL all-gather of stats)',
+                       'parallelism': f'dp{world} (TAC-major sample shards, RCCL all-gather of stats)',
+                       'driver': 'distributed.sample_posterior_sharded',
                        'hipgraph': True},
             'roofline': roof,
             'outputs_finite': finite,
             'stats_allgather_ms': round(ag_ms, 3),
         }
         if layer_ms is not None:
-            line['layer_us'] = {k: round(v[0] / max(v[1], 1) * 1e3, 2) for k, v in layer_ms.items()}
+            line['layer_us'] = layer_us(layer_ms)
         if world == 1 and not args.no_cpu_baseline:
             line['cpu_baseline'] = cpu_baseline(net.weights, cond[0])
         else:

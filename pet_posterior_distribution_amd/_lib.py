@@ -179,3 +179,40 @@ def check(rc, what=''):
 def exported_symbols():
     """Names of the C entry points this binding expects (for the load test)."""
     return [s[0] for s in SYMBOLS]
+
+
+def kernel_code_hash(symbol=b'conv_kernel', path=None):
+    """sha256 (16 hex digits) of the gfx950 code object in libpetdiff.so's .hip_fatbin that defines
+    ``symbol`` (the U-Net kernels' translation unit): it changes exactly when those kernels' machine
+    code does, so PMC counters recorded for one build can be recognised as stale for another
+    (scripts/pmc_summary.py stamps it, bench.py checks it).  None if the file has no such bundle."""
+    import hashlib
+    import struct
+    with open(path or LIB_PATH, 'rb') as f:
+        b = f.read()
+    if b[:4] != b'\x7fELF':
+        return None
+    shoff = struct.unpack_from('<Q', b, 0x28)[0]
+    shentsize, shnum, shstrndx = struct.unpack_from('<HHH', b, 0x3A)
+    secs = [struct.unpack_from('<IIQQQQIIQQ', b, shoff + i * shentsize) for i in range(shnum)]
+    stro = secs[shstrndx][4]
+    fb = None
+    for s in secs:
+        if b[stro + s[0]:b.index(b'\0', stro + s[0])] == b'.hip_fatbin':
+            fb = b[s[4]:s[4] + s[5]]
+    if fb is None:
+        return None
+    magic = b'__CLANG_OFFLOAD_BUNDLE__'
+    i = fb.find(magic)
+    while i >= 0:
+        n = struct.unpack_from('<Q', fb, i + 24)[0]
+        q = i + 32
+        for _ in range(n):
+            off, sz, idl = struct.unpack_from('<QQQ', fb, q)
+            tid = fb[q + 24:q + 24 + idl]
+            q += 24 + idl
+            co = fb[i + off:i + off + sz]
+            if sz and b'gfx950' in tid and symbol in co:
+                return hashlib.sha256(co).hexdigest()[:16]
+        i = fb.find(magic, i + 1)
+    return None

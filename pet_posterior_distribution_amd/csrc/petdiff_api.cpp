@@ -160,6 +160,7 @@ struct petdiff_ctx {
   hipStream_t split_stream = nullptr;  // second launch stream of a split generate (PETDIFF_SPLIT)
   hipEvent_t split_ev[2] = {nullptr, nullptr};
   int split = 1;
+  int seg_steps = 0;                   // reverse steps per captured graph segment (0: the whole loop)
   std::map<std::vector<int>, GraphEntry> graphs;
   // timing
   bool timing = false;
@@ -371,6 +372,7 @@ int ensure_workspace(petdiff_ctx* h, int B) {
   }
   h->graphs.clear();
   h->B_cap = B;
+  h->last_B = 0;   // the level buffers are new: nothing to read back until a forward / p_sample runs
   return PETDIFF_OK;
 }
 
@@ -656,6 +658,7 @@ int petdiff_create(const petdiff_config* cfg, const float* weights, size_t n_wei
   HIPC(hipSetDevice(device));
   HIPC(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
   if (const char* e = std::getenv("PETDIFF_SPLIT")) h->split = std::max(1, std::min(kMaxSplit, std::atoi(e)));
+  if (const char* e = std::getenv("PETDIFF_GRAPH_SEG")) h->seg_steps = std::max(0, std::atoi(e));
   if (h->split > 1) {
     HIPC(hipStreamCreateWithFlags(&h->split_stream, hipStreamNonBlocking));
     HIPC(hipEventCreateWithFlags(&h->split_ev[0], hipEventDisableTiming));
@@ -842,6 +845,9 @@ int petdiff_generate(petdiff_handle h, const float* x_T, const int32_t* tac, con
   for (int i = 0; i < n_steps; ++i)
     if (t_seq[i] < 0 || t_seq[i] >= h->T) return fail(PETDIFF_ERR_INVALID, "timestep index out of range");
   CHK(ensure_workspace(h, B));
+  // the loop overwrites the level buffers (with the fused down0 / down1, s0 / s1 / p1 end up holding the
+  // next step's data): petdiff_get_activation fails until a forward / p_sample runs again
+  h->last_B = 0;
   hipStream_t s = (hipStream_t)stream;
   const size_t xbytes = (size_t)B * h->cfg.n_roi * h->cfg.n_par * 4;
   const bool graph = use_graph && !z_all && !all_xt && !h->timing && n_steps > 0;
@@ -860,9 +866,9 @@ int petdiff_generate(petdiff_handle h, const float* x_T, const int32_t* tac, con
     tacp = h->tacbuf.as<int>();
   }
   float* bufs[2] = {h->xa.as<float>(), h->xb.as<float>()};
-  auto enqueue = [&](hipStream_t q, int k) -> int {
+  auto enqueue = [&](hipStream_t q, int k, int i0, int i1) -> int {
     const int b0 = pb[k], Bk = pb[k + 1] - pb[k];
-    for (int i = 0; i < n_steps; ++i) {
+    for (int i = i0; i < i1; ++i) {
       StepIO io{};
       io.x_in = bufs[i & 1] + (size_t)b0 * 96;
       io.t_uniform = t_seq[i];
@@ -889,37 +895,47 @@ int petdiff_generate(petdiff_handle h, const float* x_T, const int32_t* tac, con
     return PETDIFF_OK;
   };
   if (!graph) {
-    CHK(enqueue(s, 0));
+    CHK(enqueue(s, 0, 0, n_steps));
   } else {
-    hipGraphExec_t ex[kMaxSplit];
-    for (int k = 0; k < parts; ++k) {
-      std::vector<int> key{B, flag_var_tilde, tac ? 1 : 0, n_steps, parts, k};
-      key.insert(key.end(), t_seq, t_seq + n_steps);
-      auto it = h->graphs.find(key);
-      if (it == h->graphs.end()) {
-        GraphEntry ge;
-        HIPC(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
-        int rc = enqueue(h->cap_stream, k);
-        hipGraph_t g = nullptr;
-        hipError_t ee = hipStreamEndCapture(h->cap_stream, &g);
-        if (rc != PETDIFF_OK) {
-          if (g) (void)hipGraphDestroy(g);
-          return rc;
+    // The loop is captured as graph segments of seg_steps reverse steps (default: the whole loop in one):
+    // hipGraphLaunch enqueues a graph's kernel nodes on the host, so a 5000-node graph costs milliseconds
+    // of host time before its first kernel runs; with segments only the first one's enqueue is exposed,
+    // the others are enqueued while the GPU runs the earlier ones.
+    const int seg = h->seg_steps > 0 ? std::min(h->seg_steps, n_steps) : n_steps;
+    const int nseg = (n_steps + seg - 1) / seg;
+    std::vector<hipGraphExec_t> ex((size_t)parts * nseg);
+    for (int k = 0; k < parts; ++k)
+      for (int sg = 0; sg < nseg; ++sg) {
+        const int i0 = sg * seg, i1 = std::min(n_steps, i0 + seg);
+        std::vector<int> key{B, flag_var_tilde, tac ? 1 : 0, n_steps, parts, k, i0, i1};
+        key.insert(key.end(), t_seq, t_seq + n_steps);
+        auto it = h->graphs.find(key);
+        if (it == h->graphs.end()) {
+          GraphEntry ge;
+          HIPC(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
+          int rc = enqueue(h->cap_stream, k, i0, i1);
+          hipGraph_t g = nullptr;
+          hipError_t ee = hipStreamEndCapture(h->cap_stream, &g);
+          if (rc != PETDIFF_OK) {
+            if (g) (void)hipGraphDestroy(g);
+            return rc;
+          }
+          HIPC(ee);
+          ge.graph = g;
+          HIPC(hipGraphInstantiate(&ge.exec, g, nullptr, nullptr, 0));
+          it = h->graphs.emplace(key, ge).first;
         }
-        HIPC(ee);
-        ge.graph = g;
-        HIPC(hipGraphInstantiate(&ge.exec, g, nullptr, nullptr, 0));
-        it = h->graphs.emplace(key, ge).first;
+        ex[(size_t)k * nseg + sg] = it->second.exec;
       }
-      ex[k] = it->second.exec;
-    }
     if (parts == 1) {
-      HIPC(hipGraphLaunch(ex[0], s));
+      for (int sg = 0; sg < nseg; ++sg) HIPC(hipGraphLaunch(ex[sg], s));
     } else {
       HIPC(hipEventRecord(h->split_ev[0], s));
       HIPC(hipStreamWaitEvent(h->split_stream, h->split_ev[0], 0));
-      HIPC(hipGraphLaunch(ex[0], s));
-      HIPC(hipGraphLaunch(ex[1], h->split_stream));
+      for (int sg = 0; sg < nseg; ++sg) {
+        HIPC(hipGraphLaunch(ex[sg], s));
+        HIPC(hipGraphLaunch(ex[(size_t)nseg + sg], h->split_stream));
+      }
       HIPC(hipEventRecord(h->split_ev[1], h->split_stream));
       HIPC(hipStreamWaitEvent(s, h->split_ev[1], 0));
     }

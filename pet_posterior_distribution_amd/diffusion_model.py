@@ -153,6 +153,8 @@ class ImprovedDDPM:
         self._last_forward_B = 0
         self._handle = None
         self._cond_cache = None     # (unique-conditions tensor) last sent to the library
+        self._cond_cache_host = None  # its host copy when it came from a NumPy condition
+        self._inv_cache = None      # (host per-sample index, its device copy)
         self._trainer = None
         self._weights_stale = False
         self.optimizer = None
@@ -372,6 +374,7 @@ class ImprovedDDPM:
             _lib.lib().petdiff_destroy(self._handle)
             self._handle = None
             self._cond_cache = None
+            self._cond_cache_host = None
 
     def __del__(self):
         try:
@@ -390,6 +393,8 @@ class ImprovedDDPM:
         h = self._ensure_handle()
         if condition is None:
             raise NotImplementedError('the shipped UnetConditional requires a condition')
+        if not isinstance(condition, torch.Tensor) and not isinstance(tac, torch.Tensor):
+            return self._conditions_host(h, condition, B, tac)
         cond = _as_device(condition, self.device, torch.float32)
         if cond.dim() == 2:
             cond = cond[None]
@@ -402,6 +407,8 @@ class ImprovedDDPM:
             if B and (int(inv.min()) < 0 or int(inv.max()) >= cond.shape[0]):
                 raise ValueError('tac index out of range')
             uniq = cond.contiguous()
+            if cond.shape[0] == 1:
+                inv = None               # one condition: the kernels' single-condition path
         elif cond.shape[0] != B and cond.shape[0] != 1:
             raise ValueError(f'condition batch {cond.shape[0]} != x batch {B}')
         elif cond.shape[0] == 1 or bool((cond == cond[:1]).all()):
@@ -416,7 +423,49 @@ class ImprovedDDPM:
                        'petdiff_set_conditions')
             # a private copy: the caller may update its condition buffer in place between calls
             self._cond_cache = uniq.clone()
+            self._cond_cache_host = None
         return inv, uniq.shape[0]
+
+    def _conditions_host(self, h, condition, B, tac):
+        """_conditions for host (NumPy) inputs: validation, deduplication and the comparison with the
+        last condition set all run on the host, and the device copies of the unique conditions and of
+        the per-sample index are reused while their contents repeat, so a repeated call issues no copy
+        that would wait for the GPU work queued before it (a pageable host-to-device copy does)."""
+        c = np.ascontiguousarray(np.asarray(condition, dtype=np.float32))
+        if c.ndim == 2:
+            c = c[None]
+        if c.shape[1:] != (49, 54):
+            raise ValueError(f'condition must be (B, 49, 54), got {tuple(c.shape)}')
+        if tac is not None:
+            inv = np.ascontiguousarray(np.asarray(tac).reshape(-1).astype(np.int32))
+            if inv.size != B:
+                raise ValueError('tac must have one entry per sample')
+            if B and (int(inv.min()) < 0 or int(inv.max()) >= c.shape[0]):
+                raise ValueError('tac index out of range')
+            uniq = c
+            if c.shape[0] == 1:
+                inv = None               # one condition: the kernels' single-condition path
+        elif c.shape[0] != B and c.shape[0] != 1:
+            raise ValueError(f'condition batch {c.shape[0]} != x batch {B}')
+        elif c.shape[0] == 1 or bool((c == c[:1]).all()):
+            uniq, inv = c[:1], None
+        else:
+            uniq, inv = np.unique(c.reshape(c.shape[0], -1), axis=0, return_inverse=True)
+            uniq = np.ascontiguousarray(uniq.reshape(-1, 49, 54))
+            inv = np.ascontiguousarray(inv.reshape(-1).astype(np.int32))
+        hc = getattr(self, '_cond_cache_host', None)
+        if self._cond_cache is None or hc is None or hc.shape != uniq.shape or not np.array_equal(hc, uniq):
+            dev = torch.as_tensor(uniq, device=self.device)
+            _lib.check(_lib.lib().petdiff_set_conditions(h, _ptr(dev), uniq.shape[0], _stream_ptr(self.device)),
+                       'petdiff_set_conditions')
+            self._cond_cache = dev
+            self._cond_cache_host = uniq.copy()
+        if inv is None:
+            return None, uniq.shape[0]
+        ic = getattr(self, '_inv_cache', None)
+        if ic is None or ic[0].shape != inv.shape or not np.array_equal(ic[0], inv):
+            self._inv_cache = ic = (inv.copy(), torch.as_tensor(inv, device=self.device))
+        return ic[1], uniq.shape[0]
 
     def _time(self, time, B):
         t = _as_device(time, self.device, torch.int32).reshape(-1)

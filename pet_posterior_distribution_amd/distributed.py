@@ -78,30 +78,63 @@ def summarize(stats):
     return {'mean_DVR': mean[..., 0], 'mean_R1': mean[..., 1], 'std_DVR': std[..., 0], 'std_R1': std[..., 1]}
 
 
-def sample_posterior_sharded(model, cond_all, n_per_tac, seed=0, x_T_seed=1, group=None, use_graph=True):
-    """Config 4 driver: n_tac TACs x n_per_tac samples sharded TAC-major over the ranks.
+def sample_posterior_sharded(model, cond_all, n_per_tac, seed=0, x_T_seed=1, group=None, use_graph=True,
+                             return_samples=False, coll_device=None, num_timesteps=None):
+    """BASELINE configs[3] driver (main_script.py:414-436 for many test TACs at once): n_tac TACs x
+    n_per_tac posterior samples, sharded TAC-major over the ranks (global sample g = tac * n_per_tac + s).
 
-    Each rank generates its block (x_T and z from counter-based Philox keyed by the
-    global sample index, so the result does not depend on the world size), reduces it on the GPU to per-TAC Welford partials, and the
-    partials are all-gathered (RCCL) and merged.  Returns per-TAC summary dicts."""
-    import torch
+    Each rank generates its block [lo, hi) -- x_T and z from counter-based Philox keyed by g, so the
+    samples do not depend on the world size or on how ddpm_loop chunks the block -- reduces it on
+    the GPU to per-TAC Welford partials {count, mean, M2} (fp64), and the partials of all ranks are
+    all-gathered (RCCL over xGMI, or gloo) and merged with Chan's formula; a TAC that spans two ranks
+    is merged from its two partials.  ``cond_all`` is the (n_tac, 49, 54) table of every TAC, or a
+    TacTable (below) that builds only this rank's rows.
+
+    ``num_timesteps`` is ddpm_loop's (None = all T steps, as main_script.py:418-420 runs it).
+    Returns (summary dict of (n_tac, 48) arrays, merged stats (n_tac, 48, 2, 3)); with
+    ``return_samples`` also (lo, hi, this rank's samples x_0 (hi - lo, 48, 2) on the device)."""
     import torch.distributed as dist
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
-    n_tac = cond_all.shape[0]
+    dist_on = dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size(group) if dist_on else 1
+    rank = dist.get_rank(group) if dist_on else 0
+    n_tac = len(cond_all)
     lo, hi = tac_major_shards(n_tac, n_per_tac, world, rank)
     stats = np.zeros((n_tac, 48, 2, 3))
+    x0 = None
     if hi > lo:
         g = np.arange(lo, hi)
         tac_g = g // n_per_tac
         tacs = np.unique(tac_g)
-        cond = np.asarray(cond_all)[tacs]
+        cond = cond_all.rows(tacs) if hasattr(cond_all, 'rows') else np.asarray(cond_all)[tacs]
         local_tac = np.searchsorted(tacs, tac_g).astype(np.int32)
         x_T = model.philox_normal(hi - lo, seed=x_T_seed, sample_offset=lo)
-        x0 = model.ddpm_loop(x_T, cond, seed=seed, sample_offset=lo, use_graph=use_graph, tac=local_tac)
-        st = model.posterior_stats(x0, local_tac, n_tac=len(tacs))
+        x0 = model.ddpm_loop(x_T, cond, num_timesteps=num_timesteps, seed=seed, sample_offset=lo, use_graph=use_graph,
+                             tac=local_tac if len(tacs) > 1 else None)
+        st = model.posterior_stats(x0, local_tac if len(tacs) > 1 else None, n_tac=len(tacs))
         stats[tacs] = st
     if world > 1:
-        parts = allgather_stats(stats, group=group, device=model.device)
+        if coll_device is None:
+            coll_device = 'cpu' if dist.get_backend(group) == 'gloo' else model.device
+        parts = allgather_stats(stats, group=group, device=coll_device)
         stats = merge_stats(parts)
+    if return_samples:
+        return summarize(stats), stats, (lo, hi, x0)
     return summarize(stats), stats
+
+
+class TacTable:
+    """Lazily built condition table for sample_posterior_sharded: ``len`` = number of TACs, ``rows(idx)``
+    builds only the requested TACs (make(k) -> (49, 54)), so a rank never synthesises the others'."""
+
+    def __init__(self, n_tac, make):
+        self.n_tac, self.make = int(n_tac), make
+        self._rows = {}                       # built rows are kept: repeated calls reuse them
+
+    def __len__(self):
+        return self.n_tac
+
+    def rows(self, idx):
+        for k in idx:
+            if int(k) not in self._rows:
+                self._rows[int(k)] = np.asarray(self.make(int(k)), dtype=np.float32)
+        return np.stack([self._rows[int(k)] for k in idx])

@@ -250,7 +250,7 @@ class _Reader:
             raise H5Error('bad chunk B-tree node')
         level, used = self.buf[p + 5], self.u(p + 6, 2)
         q = p + 8 + 2 * self.so
-        ksz = 8 + 8 * (ndims + 1)
+        ksz = 8 + 8 * ndims                           # size, filter mask, ndims offsets (rank + 1)
         for _ in range(used):
             size, mask = self.u(q, 4), self.u(q + 4, 4)
             offs = tuple(self.u(q + 8 + 8 * i, 8) for i in range(ndims))
@@ -527,8 +527,10 @@ class _Writer:
             offs[n] = len(heap)
             heap += n.encode('utf-8') + b'\0'
             heap += b'\0' * (-len(heap) % 8)
-        heap_data = self.alloc(bytes(heap) + b'\0' * 8)
-        heap_hdr = self.alloc(b'HEAP' + bytes([0, 0, 0, 0]) + struct.pack('<QQQ', len(heap) + 8, len(heap),
+        # one 16-B free block at the end of the data segment, as the HDF5 library lays out a new heap:
+        # {offset of the next free block = 1 (H5HL_FREE_NULL, end of list), size of this block = 16}
+        heap_data = self.alloc(bytes(heap) + struct.pack('<QQ', 1, 16))
+        heap_hdr = self.alloc(b'HEAP' + bytes([0, 0, 0, 0]) + struct.pack('<QQQ', len(heap) + 16, len(heap),
                                                                          heap_data))
         per = 2 * self.LEAF_K
         groups = [names[i:i + per] for i in range(0, len(names), per)] or [[]]

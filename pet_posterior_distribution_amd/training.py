@@ -89,10 +89,12 @@ class _Mean:
 
 class WeightsCheckpoint:
     """networks.WeightsCheckpoint (networks.py:152-180): every ``every_n_epochs`` epochs save the
-    model's weights to ``root_dir/cp_<epoch>/<filename>`` (this package's .npz + .json spec; the
-    reference's ``ckpt.weights.h5`` is Keras HDF5)."""
+    model's weights to ``root_dir/cp_<epoch>/<filename>``, by default the reference's
+    ``ckpt.weights.h5`` (Keras HDF5 with the network under ``network/``, the layout
+    ``ImprovedDDPM.save_weights`` writes and ``load_weights`` reads, main_script.py:412); another
+    extension writes this package's .npz."""
 
-    def __init__(self, root_dir, every_n_epochs=1, filename='ckpt.weights.npz', overwrite=True):
+    def __init__(self, root_dir, every_n_epochs=1, filename='ckpt.weights.h5', overwrite=True):
         self.root_dir = root_dir
         self.every_n_epochs = int(every_n_epochs)
         self.filename = filename
@@ -111,8 +113,7 @@ class WeightsCheckpoint:
         path = os.path.join(sub, self.filename)
         if not self.overwrite and os.path.exists(path):
             return
-        self.model._sync_trained_weights()
-        self.model.network.save_weights(path)
+        self.model.save_weights(path)
 
 
 def check(rc, what):

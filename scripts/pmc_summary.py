@@ -22,14 +22,15 @@ def short(name):
         return LAYERS[int(m.group(1))]
     if 'down0_kernel' in name:
         return 'down0'
-    # rocprofv3 demangles conv_kernel<__bf16, 1> as 'conv_kernel<bool _Accum, int, E>'; of the 16-bit
-    # conv kinds a generate launches (0, 1, 2, 9, 10, 11) only kind 1 (down2) comes out that way
-    if 'conv_kernel<bool _Accum, int, E>' in name:
+    # rocprofv3 demangles conv_kernel<__bf16, 1, XS> as 'conv_kernel<bool _Accum, int, E, XS>' (before the
+    # XS parameter existed: 'conv_kernel<bool _Accum, int, E>'); of the 16-bit conv kinds a generate
+    # launches (0, 1, 2, 9, 10, 11) only kind 1 (down2) comes out that way
+    if re.search(r'conv_kernel<bool _Accum, int, E(, \d+)?>', name):
         return 'down2'
     return None
 
 
-def main(d, out=None, update_traffic=False):
+def main(d, out=None, update_traffic=False, dtype='bfloat16'):
     vals = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(d, 'p*', 'run_counter_collection.csv')):
         for r in csv.DictReader(open(f)):
@@ -44,17 +45,25 @@ def main(d, out=None, update_traffic=False):
             res[k]['hbm_read_bytes_corrected'] = res[k]['FETCH_SIZE'] * 2 * 1024
         if 'WRITE_SIZE' in res[k]:
             res[k]['hbm_write_bytes'] = res[k]['WRITE_SIZE'] * 1024
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    from pet_posterior_distribution_amd import _lib
+    code_hash = _lib.kernel_code_hash()       # the build these passes measured (same tree on the GPU box)
     for k in sorted(res):
         print(k, {c: round(v, 1) for c, v in res[k].items()})
+    print('kernels:', sorted(res), 'code_hash:', code_hash)
     if out:
-        json.dump(res, open(out, 'w'), indent=1)
+        json.dump(dict(res, _meta={'code_hash': code_hash, 'dtype': dtype}), open(out, 'w'), indent=1)
     if out and update_traffic:
         # bench.py's bf16 roofline reads these: update them only from passes over the default
         # (bf16, B = 1024) workload -- a --dtype bf16x3 run once overwrote them with its 3x bytes
-        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
         tp = os.path.join(root, 'profiles', 'pmc_traffic.json')
         tr = json.load(open(tp)) if os.path.exists(tp) else {}
-        for key, pre in (('up0.block', 'up0_block'), ('up0.fused', 'up0_fused')):
+        suf = {'bfloat16': '', 'bf16x3': '_bf16x3', 'float16': '_f16'}[dtype]
+        for key, pre0 in (('up0.block', 'up0_block'), ('up0.fused', 'up0_fused')):
+            pre = pre0 + suf
+            if key in res:
+                tr[pre + '_code_hash'] = code_hash
             ub = res.get(key, {})
             if 'hbm_read_bytes_corrected' in ub and 'hbm_write_bytes' in ub:
                 tr[pre + '_bytes_per_launch'] = ub['hbm_read_bytes_corrected'] + ub['hbm_write_bytes']
@@ -70,5 +79,8 @@ def main(d, out=None, update_traffic=False):
 
 
 if __name__ == '__main__':
-    args = [x for x in sys.argv[1:] if x != '--traffic']
-    main(args[0], args[1] if len(args) > 1 else None, update_traffic='--traffic' in sys.argv[1:])
+    # --traffic: update profiles/pmc_traffic.json (bench.py's PMC fields) from these passes;
+    # --dtype=bf16x3|float16: the passes ran bench.py --dtype ... (keys get a dtype suffix)
+    dt = next((x.split('=', 1)[1] for x in sys.argv[1:] if x.startswith('--dtype=')), 'bfloat16')
+    args = [x for x in sys.argv[1:] if not x.startswith('--')]
+    main(args[0], args[1] if len(args) > 1 else None, update_traffic='--traffic' in sys.argv[1:], dtype=dt)

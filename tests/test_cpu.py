@@ -417,12 +417,28 @@ def test_down1_pair_position_major_layout():
     assert sorted(pairs) == list(range(MT // 2))
 
 
-def test_bench_pmc_fields_are_bf16_passes():
-    """bench.py's roofline traffic / MFMA-busy fields (bf16 line) come from profiles/pmc_traffic.json;
-    they must be passes over the bf16 network: SQ_VALU_MFMA_BUSY_CYCLES of up0.fused equals the
-    analytic executed count (32 busy cycles per 32x32x16 MFMA of 32,768 FLOP), not bf16x3's 3x."""
+def test_bench_pmc_fields_per_dtype_and_build(monkeypatch):
+    """bench.py's roofline traffic / MFMA-busy fields come from profiles/pmc_traffic.json, per dtype: the
+    bf16 entries are passes over the bf16 network (SQ_VALU_MFMA_BUSY_CYCLES of up0.fused = the analytic
+    executed count, 32 busy cycles per 32x32x16 MFMA of 32,768 FLOP), the bf16x3 ones 3x that.  They are
+    used only when the code-object hash they were stamped with is the loaded build's
+    (_lib.kernel_code_hash); otherwise every field is None (stale counters)."""
+    import json
     import bench
-    pmc = bench.load_pmc(True)
+    from pet_posterior_distribution_amd import _lib
+    d = json.load(open(os.path.join(os.path.dirname(os.path.dirname(__file__)), 'profiles', 'pmc_traffic.json')))
     want = bench.UP0_FUSED_EXEC_FLOP_PER_SAMPLE * 1024 / 32768 * 32
-    assert pmc['mfma_busy'] is not None and abs(pmc['mfma_busy'] / want - 1) < 0.01
-    assert pmc['traffic'] is not None and pmc['traffic'] < 2.5e8
+    assert abs(d['up0_fused_mfma_busy_cycles'] / want - 1) < 0.01
+    assert d['up0_fused_bytes_per_launch'] < 2.5e8
+    if 'up0_fused_bf16x3_mfma_busy_cycles' in d:
+        assert abs(d['up0_fused_bf16x3_mfma_busy_cycles'] / (3 * want) - 1) < 0.01
+    for dt, pre in (('bfloat16', 'up0_fused'), ('bf16x3', 'up0_fused_bf16x3')):
+        stamp = d.get(pre + '_code_hash')
+        monkeypatch.setattr(_lib, 'kernel_code_hash', lambda *a, **k: stamp)
+        pmc = bench.load_pmc(True, dt)
+        if stamp is not None:
+            assert not pmc['stale'] and pmc['mfma_busy'] == d[pre + '_mfma_busy_cycles']
+        monkeypatch.setattr(_lib, 'kernel_code_hash', lambda *a, **k: 'another build')
+        pmc = bench.load_pmc(True, dt)
+        assert pmc['stale'] and pmc['mfma_busy'] is None and pmc['traffic'] is None
+        assert bench.pmc_fields(pmc, 70e-6)['mfma_util'] is None

@@ -100,3 +100,114 @@ def test_errors(tmp_path):
     h5.save_unet_h5(p, w, network_path='')
     with pytest.raises(h5.H5Error):
         h5.load_unet_h5(p, a.spec())
+
+
+def _heap_of_root(f):
+    """(data segment size, free-list head, data segment address) of the root group's local heap."""
+    r = f._r
+    for mtype, _, d in r.messages(r.root):
+        if mtype == 0x11:
+            heap = int.from_bytes(d[r.so:2 * r.so], 'little')
+            p = r.a(heap)
+            assert bytes(r.buf[p:p + 4]) == b'HEAP' and r.buf[p + 4] == 0
+            q = p + 8
+            return r.u(q, r.sl), r.u(q + r.sl, r.sl), r.u(q + 2 * r.sl, r.so)
+    raise AssertionError('root is not a symbol-table group')
+
+
+def _check_free_list(f):
+    """HDF5 local-heap free-list rules: the head is 1 (H5HL_FREE_NULL: no free block) or the offset of a
+    block {next offset, size} with size >= 2 length fields, inside the data segment; the last block's
+    next offset is 1."""
+    r = f._r
+    size, head, data = _heap_of_root(f)
+    seen = 0
+    while head != 1:
+        assert head % 8 == 0 and head + 2 * r.sl <= size, (head, size)
+        nxt, bsz = r.u(r.a(data) + head, r.sl), r.u(r.a(data) + head + r.sl, r.sl)
+        assert bsz >= 2 * r.sl and head + bsz <= size, (head, bsz, size)
+        head = nxt
+        seen += 1
+        assert seen < 1000
+    return seen
+
+
+def test_local_heap_free_list_is_valid(tmp_path):
+    """the writer's heap must follow the free-list rules libhdf5 enforces (the library-written
+    MAT file is the pin for the layout convention)."""
+    with h5.File(GOLD) as f:
+        _check_free_list(f)
+    p = str(tmp_path / 'g.h5')
+    h5.write(p, {'a': np.arange(3.0), 'b': {'c': np.ones(2, np.float32)}})
+    with h5.File(p) as f:
+        assert _check_free_list(f) == 1
+        assert f.keys() == ['a', 'b']
+
+
+def _chunked_dataset(w, arr, chunk):
+    """Object header of a chunked, deflate-compressed dataset (layout message v3 class 2, a one-level v1
+    chunk B-tree whose keys are {chunk size, filter mask, rank + 1 offsets}), written by hand."""
+    import struct
+    import zlib
+    arr = np.ascontiguousarray(arr, dtype='<f4')
+    rank = arr.ndim
+    keys, kids = [], []
+    for i0 in range(0, arr.shape[0], chunk[0]):
+        for i1 in range(0, arr.shape[1], chunk[1]):
+            blk = np.zeros(chunk, '<f4')
+            part = arr[i0:i0 + chunk[0], i1:i1 + chunk[1]]
+            blk[:part.shape[0], :part.shape[1]] = part
+            raw = zlib.compress(blk.tobytes())
+            kids.append(w.alloc(raw))
+            keys.append(struct.pack('<II', len(raw), 0) + struct.pack('<QQQ', i0, i1, 0))
+    keys.append(struct.pack('<II', 0, 0) + struct.pack('<QQQ', arr.shape[0], 0, 0))   # final key
+    body = b''.join(k + struct.pack('<Q', c) for k, c in zip(keys, kids)) + keys[-1]
+    tree = w.alloc(b'TREE' + struct.pack('<BBHQQ', 1, 0, len(kids), h5.UNDEF, h5.UNDEF) + body)
+    space = struct.pack('<BBBx4x', 1, rank, 0) + b''.join(struct.pack('<Q', s) for s in arr.shape)
+    dtype_msg = bytes([0x11, 0x20, 31, 0]) + struct.pack('<I', 4) + struct.pack('<HHBBBBI', 0, 32, 23, 8, 0, 23, 127)
+    layout = struct.pack('<BBB', 3, 2, rank + 1) + struct.pack('<Q', tree) + \
+        b''.join(struct.pack('<I', c) for c in chunk) + struct.pack('<I', 4)
+    pipeline = struct.pack('<BB6x', 1, 1) + struct.pack('<HHHH', 1, 0, 0, 1) + struct.pack('<II', 6, 0)
+    return w.object_header([w._msg(0x01, space), w._msg(0x03, dtype_msg), w._msg(0x08, layout),
+                            w._msg(0x0B, pipeline)])
+
+
+def test_chunked_deflate_dataset(tmp_path):
+    """chunk B-tree keys are 8 + 8 (rank + 1) bytes; several chunks (ragged edges) read back."""
+    import struct
+    arr = np.arange(5 * 7, dtype=np.float32).reshape(5, 7) * 0.5 - 3.0
+    w = h5._Writer()
+    w.alloc(b'\0' * 96)
+    ds = _chunked_dataset(w, arr, (2, 3))
+    root, tree_addr, heap_addr = w.group({'c': ds})
+    sb = h5.SIGNATURE + bytes([0, 0, 0, 0, 0, 8, 8, 0]) + struct.pack('<HHI', w.LEAF_K, w.NODE_K, 0)
+    sb += struct.pack('<QQQQ', 0, h5.UNDEF, len(w.out), h5.UNDEF)
+    sb += struct.pack('<QQII', 0, root, 1, 0) + struct.pack('<QQ', tree_addr, heap_addr)
+    w.out[:len(sb)] = sb
+    p = tmp_path / 'chunked.h5'
+    p.write_bytes(bytes(w.out))
+    with h5.File(str(p)) as f:
+        np.testing.assert_array_equal(f['c'].read(), arr)
+
+
+def test_weights_checkpoint_writes_reference_file(tmp_path):
+    """WeightsCheckpoint (networks.py:152-180) writes cp_<epoch>/ckpt.weights.h5 in the model-level layout
+    (network under ``network/``), which ImprovedDDPM.load_weights reads back (main_script.py:412)."""
+    from pet_posterior_distribution_amd import ImprovedDDPM
+    from pet_posterior_distribution_amd.training import WeightsCheckpoint
+    from tests.helpers import shipped_diff_args
+    a, b = _net(6), _net(7)
+    ma = ImprovedDDPM(network=a, device=0, **shipped_diff_args())
+    mb = ImprovedDDPM(network=b, device=0, **shipped_diff_args())
+    cb = WeightsCheckpoint(str(tmp_path), every_n_epochs=2)
+    cb.set_model(ma)
+    cb.on_epoch_end(0)
+    assert not (tmp_path / 'cp_1').exists()
+    cb.on_epoch_end(1)
+    path = tmp_path / 'cp_2' / 'ckpt.weights.h5'
+    assert path.exists()
+    with h5.File(str(path)) as f:
+        assert f.keys() == ['network']
+    mb.load_weights(str(path))
+    for n, _ in a.spec():
+        np.testing.assert_array_equal(b.weights[n], a.weights[n])

@@ -2,8 +2,11 @@
 
 Tolerances (written per test):
 * exact-f32 MFMA network: max|gpu - oracle_fp64| <= 1e-4 * max|oracle| (north_star: 1e-4 rtol);
-* bf16 network (fp32 accumulate): <= 3e-2 * max|oracle| on one forward;
-* fp16 network (fp32 accumulate, BASELINE config 5): <= 5e-3 * max|oracle| on one forward;
+* 16-bit networks: plain Glorot weights (no identity shortcut) and each output half (eps, v) against
+  its own magnitude, with test_gpu_parity16.py's bounds (rrms / max relative to the half's rms):
+  bf16 1.2e-2 / 0.1, fp16 1.5e-3 / 1.2e-2; 16-bit loops against f32 within one Monte-Carlo standard
+  error (test_gpu_parity16.py); the 16-bit forward / loop tests that bounded the output by a fraction
+  of its global max with identity-shortcut weights were retired in round 3 (VERDICT r02);
 * p_sample / loop with identical injected noise: posterior mean / SD within 1e-4 rtol.
 """
 import numpy as np
@@ -34,6 +37,42 @@ def rel(a, b):
     return float(np.abs(a.astype(np.float64) - b).max() / (np.abs(b).max() + 1e-30))
 
 
+# 16-bit bounds of test_gpu_parity16.py: (rrms, max error / rms), each output half on its own magnitude
+TOL16 = {'bfloat16': (1.2e-2, 0.1), 'float16': (1.5e-3, 1.2e-2)}
+
+
+def half_errors(a, b):
+    """{'eps': (rrms, max/rms), 'v': ...} of network outputs a vs b (B, 48, n_out); n_out = 2: eps only."""
+    a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+    a, b = a.astype(np.float64), np.asarray(b, np.float64)
+    out = {}
+    for k, sl in (('eps', slice(0, 2)), ('v', slice(2, 4))):
+        if b.shape[-1] <= sl.start:
+            continue
+        d, r = a[..., sl] - b[..., sl], b[..., sl]
+        rms = np.sqrt((r ** 2).mean()) + 1e-300
+        out[k] = (float(np.sqrt((d ** 2).mean()) / rms), float(np.abs(d).max() / rms))
+    return out
+
+
+def within16(a, b, dtype):
+    tr, tm = TOL16[dtype]
+    e = half_errors(a, b)
+    return all(x <= tr and y <= tm for x, y in e.values()), e
+
+
+def glorot_model(dtype, seed=17, learn_variance='learn_ranged', parameterization='eps'):
+    """Plain Glorot-uniform weights (biases U(-0.05, 0.05)), no identity shortcut."""
+    from pet_posterior_distribution_amd import ImprovedDDPM, UnetConditional
+    from pet_posterior_distribution_amd.networks import glorot_uniform_init
+    args = shipped_net_args()
+    args['learn_variance'] = learn_variance
+    net = UnetConditional(**args)
+    net.build((None, 48, 2))
+    net.weights = glorot_uniform_init(net.spec(), seed=seed, bias_scale=0.05)
+    return ImprovedDDPM(network=net, dtype=dtype, parameterization=parameterization, **shipped_diff_args())
+
+
 @pytest.fixture(scope='module')
 def conds():
     return np.stack([synthetic_condition(0), synthetic_condition(1)])
@@ -59,45 +98,6 @@ def test_unet_forward_f32(m32, conds):
     ref = R.unet_forward(m32.network.weights, x, t, cond, dt=np.float64)
     assert out.shape == (B, 48, 4)
     assert rel(out, ref) < 1e-4
-
-
-@pytest.fixture(scope='module')
-def mh16():
-    return make_model('float16')
-
-
-def test_unet_forward_fp16(mh16, conds):
-    rng = np.random.default_rng(3)
-    B = 8
-    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
-    t = np.array([999, 700, 500, 250, 17, 2, 1, 0], dtype=np.int32)
-    cond = conds[np.array([0, 1, 1, 0, 0, 1, 0, 1])]
-    out = mh16.call({'x': x, 'time': t, 'condition': cond})
-    ref = R.unet_forward(mh16.network.weights, x, t, cond, dt=np.float64)
-    assert rel(out, ref) < 5e-3
-
-
-def test_fp16_loop_statistics_vs_f32(mh16, m32, conds):
-    """fp16 network vs exact-f32 network on the same counter-based noise (100-step loop)."""
-    rng = np.random.default_rng(12)
-    B = 256
-    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
-    a = mh16.ddpm_loop(x, conds[:1], num_timesteps=100, seed=5).cpu().numpy()
-    b = m32.ddpm_loop(x, conds[:1], num_timesteps=100, seed=5).cpu().numpy()
-    assert np.isfinite(a).all()
-    scale = np.abs(b).mean()
-    assert np.abs(a.mean(0) - b.mean(0)).max() < 0.05 * scale
-
-
-def test_unet_forward_bf16(m16, conds):
-    rng = np.random.default_rng(2)
-    B = 8
-    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
-    t = np.array([999, 700, 500, 250, 17, 2, 1, 0], dtype=np.int32)
-    cond = np.repeat(conds[:1], B, 0)
-    out = m16.call({'x': x, 'time': t, 'condition': cond})
-    ref = R.unet_forward(m16.network.weights, x, t, cond, dt=np.float64)
-    assert rel(out, ref) < 3e-2
 
 
 @pytest.mark.parametrize('B', [1, 5, 37])
@@ -278,18 +278,6 @@ def test_batch_above_max_rejected(m16, conds):
         m16.ddpm(x, np.zeros(_lib.MAX_BATCH + 1, np.int32), conds[:1])
 
 
-def test_bf16_loop_statistics_vs_f32(m16, m32, conds):
-    """bf16 network vs exact-f32 network on the same noise: posterior moments agree statistically."""
-    rng = np.random.default_rng(10)
-    B = 256
-    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
-    a = m16.ddpm_loop(x, conds[:1], num_timesteps=100, seed=5).cpu().numpy()
-    b = m32.ddpm_loop(x, conds[:1], num_timesteps=100, seed=5).cpu().numpy()
-    assert np.isfinite(a).all()
-    scale = np.abs(b).mean()
-    assert np.abs(a.mean(0) - b.mean(0)).max() < 0.1 * scale
-
-
 def test_posterior_stats(m32):
     rng = np.random.default_rng(11)
     B = 1000
@@ -416,17 +404,18 @@ def test_split_streams_bitwise(conds, monkeypatch):
     two.close()
 
 
-@pytest.mark.parametrize('dtype,tol', [('bfloat16', 3e-2), ('float16', 5e-3)])
-def test_fused_up_levels_forward(conds, dtype, tol, monkeypatch):
+@pytest.mark.parametrize('dtype', ['bfloat16', 'float16'])
+def test_fused_up_levels_forward(conds, dtype, monkeypatch):
     """Fused up levels (k2 conv composed into the block conv, 2-phase 4-tap GEMM on the coarse
-    input + left-edge correction, u-path maps through the block) against the oracle and against
-    the separate-launch path (PETDIFF_FUSE_UP=0): ragged batches, conditions interleaved per
-    sample (the epilogue's per-row map path), per-sample t."""
+    input + left-edge correction, u-path maps through the block) against the fp64 oracle and against
+    the separate-launch path (PETDIFF_FUSE_UP=0), Glorot weights, each output half on its own
+    magnitude (TOL16): ragged batches, conditions interleaved per sample (the epilogue's per-row map
+    path), per-sample t."""
     monkeypatch.setenv('PETDIFF_FUSE_UP', '0')
-    plain = make_model(dtype, seed=13)
+    plain = glorot_model(dtype, seed=13)
     plain._ensure_handle()
     monkeypatch.setenv('PETDIFF_FUSE_UP', '1')
-    fused = make_model(dtype, seed=13)
+    fused = glorot_model(dtype, seed=13)
     fused._ensure_handle()
     table = np.stack([conds[0], conds[1], conds[0] * 0.9 + 0.05])
     for B in (1, 5, 37, 96):
@@ -437,33 +426,47 @@ def test_fused_up_levels_forward(conds, dtype, tol, monkeypatch):
         ref = R.unet_forward(fused.network.weights, x, t, cond, dt=np.float64)
         a = fused.call({'x': x, 'time': t, 'condition': cond})
         b = plain.call({'x': x, 'time': t, 'condition': cond})
-        assert rel(a, ref) < tol, (B, rel(a, ref))
-        assert rel(b, ref) < tol
-        assert rel(a, b.cpu().numpy().astype(np.float64)) < tol
+        for got in (a, b):
+            ok, e = within16(got, ref, dtype)
+            assert ok, (B, e)
+        ok, e = within16(a, b.cpu().numpy(), dtype)
+        assert ok, (B, 'fused vs unfused', e)
     plain.close()
     fused.close()
 
 
-def test_fused_up_loop_vs_unfused(conds, monkeypatch):
-    """bf16 loop (graph, fused next-step down0, one condition -> the LDS map path) with and
-    without the fused up levels: posterior moments agree; both deterministic."""
+def test_fused_up_loop_vs_unfused(monkeypatch):
+    """bf16 loop (graph, fused next-step down0 / down1, one condition -> the LDS map path) with and
+    without the fused up levels, on the briefly trained network (tests.helpers.quick_trained_weights:
+    an eps-predictor whose chain stays bounded with no identity shortcut): both deterministic; per-ROI
+    posterior mean and SD within one Monte-Carlo standard error of each other (the two differ by bf16
+    rounding only: u is not rounded in the fused path, the composite weights are rounded once)."""
+    from tests.helpers import quick_trained_weights
+    from pet_posterior_distribution_amd import ImprovedDDPM, UnetConditional
+    W, cond = quick_trained_weights()
+
+    def mk():
+        net = UnetConditional(**shipped_net_args())
+        net.build((None, 48, 2))
+        net.weights = W
+        m = ImprovedDDPM(network=net, dtype='bfloat16', **shipped_diff_args())
+        m._ensure_handle()
+        return m
     monkeypatch.setenv('PETDIFF_FUSE_UP', '0')
-    plain = make_model('bfloat16', seed=14)
-    plain._ensure_handle()
+    plain = mk()
     monkeypatch.setenv('PETDIFF_FUSE_UP', '1')
-    fused = make_model('bfloat16', seed=14)
-    fused._ensure_handle()
-    rng = np.random.default_rng(25)
-    B = 256
-    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
-    a = fused.ddpm_loop(x, conds[:1], num_timesteps=100, seed=6).cpu().numpy()
-    a2 = fused.ddpm_loop(x, conds[:1], num_timesteps=100, seed=6).cpu().numpy()
-    b = plain.ddpm_loop(x, conds[:1], num_timesteps=100, seed=6).cpu().numpy()
+    fused = mk()
+    B = 512
+    x = fused.philox_normal(B, seed=25)
+    a = fused.ddpm_loop(x, cond[None], num_timesteps=100, seed=6).cpu().numpy()
+    a2 = fused.ddpm_loop(x, cond[None], num_timesteps=100, seed=6).cpu().numpy()
+    b = plain.ddpm_loop(x, cond[None], num_timesteps=100, seed=6).cpu().numpy()
     np.testing.assert_array_equal(a, a2)
     assert np.isfinite(a).all()
-    scale = np.abs(b).mean()
-    assert np.abs(a.mean(0) - b.mean(0)).max() < 0.1 * scale
-    assert np.abs(a.std(0) - b.std(0)).max() < 0.1 * b.std(0).mean()
+    sd = b.std(0)
+    assert (sd > 0).all()
+    assert (np.abs(a.mean(0) - b.mean(0)) <= sd * np.sqrt(2.0 / B)).all()
+    assert (np.abs(a.std(0) / sd - 1) <= np.sqrt(1.0 / B)).all()
     plain.close()
     fused.close()
 
@@ -471,10 +474,10 @@ def test_fused_up_loop_vs_unfused(conds, monkeypatch):
 @pytest.mark.parametrize('lv,param', [('learn_ranged', 'eps'), ('', 'eps'), ('learn_ranged', 'v')])
 def test_p_sample_bf16_fused_levels(conds, lv, param):
     """p_sample through the 16-bit network (fused up levels; the final conv + p_sample epilogue
-    writing mean / var / var_tilde).  The bf16 network output is checked against the fp64 oracle
-    network (3e-2), and the fp32 p_sample epilogue against the oracle's p_mean_variance applied
+    writing mean / var / var_tilde), Glorot weights.  The bf16 network output is checked against the
+    fp64 oracle network (each half on its own magnitude, TOL16), and the fp32 p_sample epilogue against the oracle's p_mean_variance applied
     to that same network output (1e-4); t = 0 exactly noise-free; per-sample conditions and t."""
-    m = make_model('bfloat16', seed=6, learn_variance=lv, parameterization=param, final_scale=0.2)
+    m = glorot_model('bfloat16', seed=6, learn_variance=lv, parameterization=param)
     rng = np.random.default_rng(26)
     B = 9
     x = rng.standard_normal((B, 48, 2)).astype(np.float32)
@@ -483,7 +486,8 @@ def test_p_sample_bf16_fused_levels(conds, lv, param):
     table = np.stack([conds[0], conds[1]])
     cond = table[rng.integers(0, 2, B)]
     net = m.call({'x': x, 'time': t, 'condition': cond}).cpu().numpy().astype(np.float64)
-    assert rel(net, R.unet_forward(m.network.weights, x, t, cond, dt=np.float64)) < 3e-2
+    ok, e = within16(net, R.unet_forward(m.network.weights, x, t, cond, dt=np.float64), 'bfloat16')
+    assert ok, e
     mean, var, var_t = m.ddpm(x, t, cond, z=z)
     out = R.p_mean_variance(S, net, x.astype(np.float64), t, lv, param, dt=np.float64)
     mask = np.where(t == 0, 0., 1.).reshape(-1, 1, 1)
