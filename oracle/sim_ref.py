@@ -4,7 +4,7 @@ TEST INFRASTRUCTURE ONLY (see oracle/iddpm_ref.py header).
 
 Restates sample_sim_data.py:139-215 (+ helper_func.py:146-162) with the generator's
 counter-based stream: helper_func.truncnormal_samples as whole-vector rejection of
-MvNormal draws (mu + L z, L = cholesky(Cov)); SRTM2 activity = create_activity_curve *
+MvNormal draws (mu + L z, L = cholesky_psd(Cov), a semi-definite Cholesky); SRTM2 activity = create_activity_curve *
 dt (kinetic_model.py:142-158 via oracle/srtm2_ref.srtm2_tac, pinned to the
 reference's outputs); a negative TAC redraws (DVR, R1, ref) (sample_sim_data.py:175-181);
 noise noisy/dt = x/dt + sqrt(x/dt) TN(0, sigma, low = -sqrt(x/dt)) by rejection.
@@ -40,9 +40,29 @@ def draw_truncated_mvn(seed, g, purpose, outer, mu, L):
     return x, -1
 
 
+def cholesky_psd(A):
+    """Lower factor L, L L^T = A, of a positive SEMI-definite A (the GPU generator's, sim_kernels.hip):
+    pivots <= 1e-12 max diag(A) give zero columns (the reference's Cov_tac_ref has rank 49 of 54;
+    np.random.multivariate_normal at helper_func.py:158 accepts it)."""
+    A = np.asarray(A, dtype=np.float64)
+    n = A.shape[0]
+    tol = 1e-12 * np.diag(A).max()
+    L = np.zeros_like(A)
+    for i in range(n):
+        for j in range(i + 1):
+            s = A[i, j] - L[i, :j] @ L[j, :j]
+            if i == j:
+                if s < -1e-8 * np.diag(A).max():
+                    raise np.linalg.LinAlgError('not positive semi-definite')
+                L[i, i] = np.sqrt(s) if s > tol else 0.0
+            else:
+                L[i, j] = s / L[j, j] if L[j, j] > 0 else 0.0
+    return L
+
+
 def simulate_sample(P, seed, g):
     """One sample g: dict(DVR, R1, ref, tac (48, 54) activity, noisy (48, 54) activity)."""
-    LD, LR, LC = (np.linalg.cholesky(P[k]) for k in ('Cov_DVR', 'Cov_R1', 'Cov_tac_ref'))
+    LD, LR, LC = (cholesky_psd(P[k]) for k in ('Cov_DVR', 'Cov_R1', 'Cov_tac_ref'))
     tv, dt = P['time_vector'], P['dt']
     for outer in range(MAX_OUTER):
         dvr, _ = draw_truncated_mvn(seed, g, 0, outer, P['mu_DVR'], LD)

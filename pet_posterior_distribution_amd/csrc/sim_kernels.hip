@@ -168,18 +168,27 @@ int fail(const std::string& m, int code = 1) {
   return code;
 }
 
-// lower Cholesky factor (row-major); false if not SPD
+// Lower Cholesky factor L (row-major) of a symmetric positive SEMI-definite A, L L^T = A: a pivot
+// s <= 1e-12 max diag(A) is a direction of (numerically) zero variance, so its column of L is zero.
+// The reference's Cov_tac_ref (prior_stats_nROI48) has rank 49 of 54 and np.random.multivariate_normal
+// (helper_func.py:158) accepts it (SVD factor); this factor draws the same distribution.
+// false if A is not positive semi-definite (a pivot below -tol) or not finite.
 bool cholesky(const double* A, int n, std::vector<double>& L) {
   L.assign((size_t)n * n, 0.0);
+  double dmax = 0.0;
+  for (int i = 0; i < n; ++i) dmax = std::max(dmax, A[(size_t)i * n + i]);
+  const double tol = 1e-12 * dmax;
+  if (!(dmax > 0.0) || !std::isfinite(dmax)) return false;
   for (int i = 0; i < n; ++i)
     for (int j = 0; j <= i; ++j) {
       double s = A[(size_t)i * n + j];
       for (int k = 0; k < j; ++k) s -= L[(size_t)i * n + k] * L[(size_t)j * n + k];
       if (i == j) {
-        if (s <= 0.0) return false;
-        L[(size_t)i * n + i] = std::sqrt(s);
+        if (!std::isfinite(s) || s < -1e-8 * dmax) return false;
+        L[(size_t)i * n + i] = s > tol ? std::sqrt(s) : 0.0;
       } else {
-        L[(size_t)i * n + j] = s / L[(size_t)j * n + j];
+        const double d = L[(size_t)j * n + j];
+        L[(size_t)i * n + j] = d > 0.0 ? s / d : 0.0;
       }
     }
   return true;
@@ -232,7 +241,7 @@ int petsim_generate(const petsim_prior* p, uint64_t seed, uint64_t sample_offset
   if (n == 0) return 0;
   std::vector<double> LD, LR, LC;
   if (!cholesky(p->cov_DVR, NR, LD) || !cholesky(p->cov_R1, NR, LR) || !cholesky(p->cov_ref, NF, LC))
-    return fail("prior covariance is not positive definite");
+    return fail("prior covariance is not positive semi-definite");
   std::vector<double> t(p->time_vector, p->time_vector + NF);
   std::set<double> uniq(t.begin(), t.end());
   if ((int)uniq.size() * 2 != NG) return fail("frame times must be 54 distinct values");

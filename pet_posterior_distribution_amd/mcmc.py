@@ -79,7 +79,9 @@ class MetropolisSRTM2:
     def run(self, n_chains, draws, tune, seed=0, x0=None, return_chains=False, return_draws=False):
         """pm.sample(draws, tune, step=Metropolis(NormalProposal)) (mcmc.py:156-157) over n_chains chains.
         return_draws: also keep the trace (the reference's idata, mcmc.py:162-164) as
-        res['draws'], a CUDA fp64 tensor (n_chains, draws, 96) = [DVR | R1]."""
+        res['draws'], a CUDA fp64 tensor (n_chains, draws, 96) = [DVR | R1], and its convergence check
+        (mcmc.py:183-194) as res['convergence'] (metrics.convergence_report: R-hat per ROI, rhat_max, and
+        the reference's flag R-hat > 1.02)."""
         x0t = None if x0 is None else torch.as_tensor(np.asarray(x0), dtype=torch.float64,
                                                        device=self.device).reshape(n_chains, 96).contiguous()
         stats = torch.empty((n_chains, 96, 3), dtype=torch.float64, device=self.device)
@@ -104,6 +106,10 @@ class MetropolisSRTM2:
                'chain_draws_per_s': n_chains * (draws + tune) / elapsed if elapsed > 0 else float('inf')}
         if return_draws:
             res['draws'] = trace
+            if draws >= 4 and n_chains >= 1:
+                # mcmc.py:183-194: rank-normalised split R-hat per ROI; flag = any R-hat > 1.02
+                from .metrics import convergence_report
+                res['convergence'] = convergence_report(trace)
         if return_chains:
             res['chain_stats'] = st
             res['last'] = last.cpu().numpy()

@@ -148,3 +148,62 @@ def ess_pair(nn_samples, mcmc_draws):
     ess_mcmc = effective_sample_size(np.moveaxis(tmp, 0, -1), cross_chain_dims=-1)
     ess_nn = effective_sample_size(nn)
     return {'MCMC': ess_mcmc, 'NN': ess_nn}
+
+
+# ------------------------------------------------------------------ MCMC convergence (mcmc.py:183-194)
+RHAT_FLAG = 1.02          # mcmc.py:188: runs with R-hat above this are logged as possibly not converged
+
+
+def _split_chains(x):
+    """(chains, draws, ...) -> (2 chains, draws // 2, ...): each chain's first and last halves (an odd
+    middle draw is dropped), as ArviZ's _split_chains."""
+    half = x.shape[1] // 2
+    return np.concatenate([x[:, :half], x[:, x.shape[1] - half:]], axis=0)
+
+
+def _z_scale(x):
+    """Rank normalisation over all draws of all chains (axes 0, 1; average ranks for ties), then the
+    normal quantile of (rank - 3/8) / (S + 1/4) (Vehtari et al. 2021, eq. 14; ArviZ's _z_scale)."""
+    from scipy.stats import norm, rankdata
+    flat = x.reshape((x.shape[0] * x.shape[1],) + x.shape[2:])
+    r = rankdata(flat, method='average', axis=0).reshape(x.shape)
+    return norm.ppf((r - 0.375) / (flat.shape[0] + 0.25))
+
+
+def _rhat_basic(x):
+    """Gelman-Rubin R-hat of (chains, draws, ...): sqrt((B / W + n - 1) / n) with B = n var(chain means),
+    W = mean within-chain variance (ddof = 1 both)."""
+    n = x.shape[1]
+    b = n * np.var(x.mean(axis=1), axis=0, ddof=1)
+    w = np.mean(np.var(x, axis=1, ddof=1), axis=0)
+    return np.sqrt((b / w + n - 1) / n)
+
+
+def rhat(draws):
+    """pm.rhat (PyMC 5.12 -> ArviZ ``rhat(method='rank')``; not vendored here, so this restates the
+    published algorithm, Vehtari et al. 2021): per scalar parameter, the maximum of the rank-normalised
+    split R-hat of the draws (bulk) and of their folded values |x - median| (tail).  A parameter whose
+    draws are constant or not finite gets NaN.
+
+    draws: (chains, draws, n_params) -> (n_params,) float64."""
+    x = np.asarray(draws.cpu().numpy() if isinstance(draws, torch.Tensor) else draws, dtype=np.float64)
+    if x.ndim == 2:
+        x = x[..., None]
+    s = _split_chains(x)
+    bulk = _rhat_basic(_z_scale(s))
+    med = np.median(s.reshape(-1, s.shape[2]), axis=0)
+    tail = _rhat_basic(_z_scale(np.abs(s - med)))
+    out = np.maximum(bulk, tail)
+    bad = ~np.isfinite(s).all(axis=(0, 1)) | (np.ptp(s.reshape(-1, s.shape[2]), axis=0) == 0)
+    out[bad] = np.nan
+    return out
+
+
+def convergence_report(draws, n_roi=48, threshold=RHAT_FLAG):
+    """mcmc.py:183-194: R-hat of var_DVR and var_R1 from the trace (chains, draws, 2 n_roi) = [DVR | R1];
+    ``flag`` is the reference's 'rhat > 1.02' condition (it then logs the file name and rhat_max)."""
+    r = rhat(draws)
+    rd, rr = r[:n_roi], r[n_roi:2 * n_roi]
+    mx = float(np.nanmax(r))
+    return {'rhat_DVR': rd, 'rhat_R1': rr, 'rhat_max': mx,
+            'flag': bool(np.any(rd > threshold) or np.any(rr > threshold)), 'threshold': threshold}

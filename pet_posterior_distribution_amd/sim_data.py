@@ -10,9 +10,12 @@ tests have realistic conditions without the Git-LFS test set:
 * ``make_condition`` -- condition rows [tac_noisy/dt (48 ROIs) | tac_ref] as in
   main_script.py:110-113.
 
-The reference's ``prior_stats_nROI48.pik`` is a pickle and is deliberately NOT
-loaded (no unpickling of reference files); ``synthetic_prior`` draws prior
-statistics of the same shapes from a fixed seed instead.
+The prior is the reference's own (``reference_prior``): the arrays of
+``prior_stats_nROI48.pik`` (sample_sim_data.py:106-126, mcmc.py:84-93), shipped as
+``data/prior_stats_nROI48.npz``.  They were extracted by tests/golden/make_golden.py,
+which parses the pickle's byte stream with a disassembler and rebuilds only literal
+data (no unpickling of reference files).  ``synthetic_prior`` (the rounds 1-2
+default, seeded synthetic statistics of the same shapes) stays for the G2 fixture.
 """
 from __future__ import annotations
 
@@ -53,6 +56,22 @@ def reference_tac(time_vector):
     """Smooth cerebellum-like reference TAC (arbitrary units, synthetic)."""
     t = np.asarray(time_vector, dtype=np.float64)
     return 1.2 * (t / 1.5) * np.exp(1 - t / 1.5) + 0.35 * np.exp(-t / 70.0) * (1 - np.exp(-t / 0.8))
+
+
+_REF_PRIOR = None
+
+
+def reference_prior():
+    """The reference's prior statistics (prior_stats_nROI48.pik): mu_DVR, Cov_DVR, mu_R1, Cov_R1 (48),
+    mu_k2p, mu_tac_ref, Cov_tac_ref (54) as float64 arrays, ROI_names; the default prior of every
+    generator here (the data the reference's test TACs, training set and MCMC priors come from)."""
+    global _REF_PRIOR
+    if _REF_PRIOR is None:
+        import os
+        with np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'data', 'prior_stats_nROI48.npz')) as z:
+            _REF_PRIOR = {k: (z[k].astype(np.float64) if z[k].dtype.kind == 'f' else z[k]) for k in z.files}
+        _REF_PRIOR['mu_k2p'] = np.float64(_REF_PRIOR['mu_k2p'])
+    return {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in _REF_PRIOR.items()}
 
 
 def synthetic_prior(seed=2025):
@@ -114,7 +133,7 @@ def noisy_tac(tac, dt, time_vector, sigma_roi, rng):
 
 def make_condition(seed=0, prior=None, mean_sigma_noise=0.1, return_truth=False):
     """One synthetic test TAC -> condition (49, 54) float32 (main_script.py:110-113)."""
-    prior = prior or synthetic_prior()
+    prior = prior or reference_prior()
     rng = np.random.default_rng(seed)
     tv, dt = time_grid()
     while True:
@@ -139,7 +158,7 @@ def make_condition(seed=0, prior=None, mean_sigma_noise=0.1, return_truth=False)
 def mh_problem(seed=0, prior=None, mean_sigma_noise=0.1):
     """The MH inputs of one synthetic test TAC (mcmc.py:73-137): frame times, reference
     TAC, fixed k2', y_obs, per-frame noise sigmas and the MvNormal priors."""
-    prior = prior or synthetic_prior()
+    prior = prior or reference_prior()
     cond, truth = make_condition(seed, prior, mean_sigma_noise, return_truth=True)
     return dict(time_vector=truth['time_vector'], tac_ref=truth['tac_ref'], k2p=float(truth['k2p']),
                 y_obs=cond[:N_ROI].astype(np.float64), sigma_noise=truth['sigma_noise'],
@@ -169,7 +188,7 @@ def simulate_dataset(n, prior=None, mean_sigma_noise=0.1, seed=0, sample_offset=
     import torch
 
     from . import _lib
-    prior = prior or synthetic_prior()
+    prior = prior or reference_prior()
     tv, dt = time_grid()
     if sigma_noise is None:
         sigma_noise = dataset_sigma_noise(mean_sigma_noise, np.random.default_rng(seed))

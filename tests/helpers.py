@@ -9,7 +9,9 @@ def synthetic_condition(seed=0):
 
 def mh_problem(g2, case=0, noise=0.1, seed=0):
     """One TAC's MH problem (mcmc.py:73-137 inputs) built from the golden SRTM2 case:
-    y = SRTM2 truth + sqrt(tac)-scaled Gaussian noise, synthetic MvN priors."""
+    y = SRTM2 truth + sqrt(tac)-scaled Gaussian noise, synthetic MvN priors (the G2 cases are drawn from sim_data.synthetic_prior; the reference's
+    prior covariances have condition numbers up to 1e7, which puts the chain-path equality tests'
+    accept / reject decisions at the mercy of last-bit differences in the quadratic form)."""
     import numpy as np
     from oracle import srtm2_ref as K
     from pet_posterior_distribution_amd.sim_data import synthetic_prior

@@ -442,3 +442,52 @@ def test_bench_pmc_fields_per_dtype_and_build(monkeypatch):
         pmc = bench.load_pmc(True, dt)
         assert pmc['stale'] and pmc['mfma_busy'] is None and pmc['traffic'] is None
         assert bench.pmc_fields(pmc, 70e-6)['mfma_util'] is None
+
+
+def test_reference_prior_fixture():
+    """G0: the arrays of the reference's prior_stats_nROI48.pik (sample_sim_data.py:106-126), read by
+    tests/golden/make_golden.py without unpickling; the package ships an identical copy
+    (sim_data.reference_prior), the default prior of the generators, MH problems and the bench TAC.
+    Structural pins: SURVEY 2 (48 ROIs, 54 frames, mu_k2p = 0.0126, ROI_names), symmetric positive
+    definite covariances."""
+    from pet_posterior_distribution_amd.sim_data import reference_prior
+    g = np.load(os.path.join(os.path.dirname(__file__), 'golden', 'g0_prior.npz'))
+    p = reference_prior()
+    assert sorted(g.files) == sorted(p)
+    for k in g.files:
+        np.testing.assert_array_equal(np.asarray(p[k]), g[k])
+    assert p['mu_DVR'].shape == (48,) and p['Cov_R1'].shape == (48, 48) and p['Cov_tac_ref'].shape == (54, 54)
+    assert abs(float(p['mu_k2p']) - 0.0126) < 1e-9 and p['ROI_names'][0] == 'Hippocampus' and len(set(p['ROI_names'])) == 48
+    from oracle.sim_ref import cholesky_psd
+    for c in ('Cov_DVR', 'Cov_R1', 'Cov_tac_ref'):
+        np.testing.assert_allclose(p[c], p[c].T, rtol=0, atol=0)
+        ev = np.linalg.eigvalsh(p[c])
+        assert ev.min() > -1e-12 * ev.max()                   # positive semi-definite
+        L = cholesky_psd(p[c])                                 # the generators' factor
+        assert np.abs(L @ L.T - p[c]).max() < 1e-13 * np.abs(p[c]).max()
+    assert np.linalg.matrix_rank(p['Cov_tac_ref']) < 54       # rank-deficient: a plain Cholesky fails
+    assert (p['mu_DVR'] > 0).all() and (p['mu_R1'] > 0).all()
+
+
+def test_static_pickle_reader_rejects_code():
+    """make_golden.read_pickle_data rebuilds literal data only: a pickle that references anything but
+    numpy's array / dtype / scalar reconstruction is refused (nothing is imported or called)."""
+    import pickle
+    import sys
+    import tempfile
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), 'golden'))
+    from make_golden import read_pickle_data
+    with tempfile.TemporaryDirectory() as d:
+        ok = os.path.join(d, 'ok.pik')
+        with open(ok, 'wb') as f:
+            pickle.dump({'a': np.arange(6.0).reshape(2, 3), 'b': [1, 'x'], 's': np.float64(2.5),
+                         'f': np.asfortranarray(np.eye(2, 3, dtype=np.float32))}, f)
+        got = read_pickle_data(ok)
+        np.testing.assert_array_equal(got['a'], np.arange(6.0).reshape(2, 3))
+        np.testing.assert_array_equal(got['f'], np.eye(2, 3, dtype=np.float32))
+        assert got['b'] == [1, 'x'] and got['s'] == 2.5
+        bad = os.path.join(d, 'bad.pik')
+        with open(bad, 'wb') as f:
+            pickle.dump({'x': os.getcwd}, f)           # a reference to a callable: refused
+        with pytest.raises(ValueError):
+            read_pickle_data(bad)

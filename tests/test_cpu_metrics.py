@@ -41,3 +41,58 @@ def test_ess_cross_chain_iid():
     ess = effective_sample_size(x, cross_chain_dims=-1)
     assert ess.shape == (4,)
     assert np.all(np.abs(ess / 10000 - 1) < 0.15)
+
+
+def _rhat_reference_loop(x):
+    """Straight restatement of Vehtari et al. (2021) rank-normalised split R-hat, one parameter at a time
+    (ranks by argsort with explicit tie averaging), to pin metrics.rhat's vectorised form."""
+    from scipy.stats import norm
+    out = []
+    for p in range(x.shape[2]):
+        c = x[..., p]
+        h = c.shape[1] // 2
+        s = np.concatenate([c[:, :h], c[:, c.shape[1] - h:]], 0)
+
+        def z(a):
+            flat = a.reshape(-1)
+            order = np.argsort(flat, kind='mergesort')
+            ranks = np.empty(flat.size)
+            i = 0
+            while i < flat.size:
+                j = i
+                while j + 1 < flat.size and flat[order[j + 1]] == flat[order[i]]:
+                    j += 1
+                ranks[order[i:j + 1]] = (i + j) / 2 + 1
+                i = j + 1
+            return norm.ppf((ranks.reshape(a.shape) - 0.375) / (flat.size + 0.25))
+
+        def basic(a):
+            n = a.shape[1]
+            B = n * a.mean(1).var(ddof=1)
+            W = a.var(1, ddof=1).mean()
+            return np.sqrt(((n - 1) / n * W + B / n) / W)
+        out.append(max(basic(z(s)), basic(z(np.abs(s - np.median(s))))))
+    return np.array(out)
+
+
+def test_rhat_rank_normalised_split():
+    """pm.rhat = ArviZ rank-normalised split R-hat (mcmc.py:186-187; ArviZ not vendored: pinned to the
+    published formulas, parity with ArviZ itself unpinned).  Mixed chains -> ~1; one shifted chain -> above
+    the reference's 1.02 flag; a scale difference is caught by the folded (tail) R-hat; odd draw counts
+    and ties handled; the vectorised form equals a per-parameter restatement."""
+    from pet_posterior_distribution_amd.metrics import rhat, convergence_report
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((4, 1001, 6))
+    x[..., 5] = np.round(x[..., 5])                     # heavy ties
+    np.testing.assert_allclose(rhat(x), _rhat_reference_loop(x), rtol=1e-12)
+    assert np.abs(rhat(x)[:5] - 1).max() < 0.01
+    y = x.copy()
+    y[0, :, 1] += 1.0                                    # one chain off in location
+    y[1, :, 2] *= 3.0                                    # one chain off in scale only
+    r = rhat(y)
+    assert r[1] > 1.05 and r[2] > 1.02
+    np.testing.assert_allclose(r, _rhat_reference_loop(y), rtol=1e-12)
+    t = np.concatenate([x[:, :, :4], y[:, :, 1:5]], axis=2)    # 8 "ROI" pairs layout [DVR | R1], n_roi = 4
+    rep = convergence_report(t, n_roi=4)
+    assert rep['flag'] and rep['rhat_max'] == np.nanmax(rhat(t))
+    assert not convergence_report(np.concatenate([x[:, :, :4], x[:, :, :4]], 2), n_roi=4)['flag']
