@@ -152,8 +152,8 @@ struct petdiff_ctx {
   // run the next step's down0 inside the previous step's up2.block epilogue (generate);
   // PETDIFF_FUSE_DOWN0=0 restores the standalone down0 launch per step (A/B switch)
   bool fuse_down0 = true;
-  // ... and the next step's down1 too (bf16, one condition; PETDIFF_FUSE_DOWN1=0: standalone launch).
-  // Bitwise equal; +0.3..0.8 % end to end in three A/B calls (unet_kernels.hip, fused_down1)
+  // ... and the next step's down1 too (16-bit networks; PETDIFF_FUSE_DOWN1=0: standalone launch).
+  // Bitwise equal; bf16: +0.3..0.8 % end to end in three A/B calls (unet_kernels.hip, fused_down1)
   bool fuse_down1 = true;
   DevBuf xa, xb, tacbuf, tbuf, rng;
   hipStream_t cap_stream = nullptr;
@@ -447,8 +447,10 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
   d0.p0 = p0;
   d0.B = B;
   if (!io.skip_down0) CHK(timed(0, [&] { return launch_down0<T>(d0, s, h->x3); }));
-  // fused down1 (16-bit bf16 network, one condition): the previous step's epilogue wrote s1 / p1
-  const bool d1_fuse = io.d1_ok && std::is_same<T, bf16>::value && !h->x3 && h->fuse_up && io.tac == nullptr;
+  // fused down1 (16-bit networks: bf16, fp16, bf16x3; any conditions): the previous step's epilogue wrote
+  // s1 / p1.  The kernel runs it on every tile whenever d1_w is set (tiles with several conditions read
+  // per-sample maps), so the host's decision to skip the launch is the only one
+  const bool d1_fuse = io.d1_ok && sizeof(T) == 2 && h->fuse_up;
 
   struct LIO { const void* s1; int c1; const void* s2; int c2; void* out; void* pool; };
   const LIO lio[kNumConvLayers] = {

@@ -62,12 +62,12 @@ struct FinalArgs {
   // epilogue also runs down0 on x_next for its own samples (writing next.s0 / next.p0),
   // which removes the down0 launch from every step but the first.
   Down0Args next;
-  // Fused down1 of the NEXT reverse step (bf16, one condition, with `next`): when d1_w is set the
-  // epilogue also runs down1 (Conv1D 128 -> 256, k6 + res, MaxPool) on its own samples' p0, so the
-  // down1 launch leaves every step but the first.  d1_w: down1's packed weights (wpack layout).
+  // Fused down1 of the NEXT reverse step (16-bit networks, with `next`): when d1_w is set the epilogue
+  // also runs down1 (Conv1D 128 -> 256, k6 + res, MaxPool) on its own samples' p0, so the down1 launch
+  // leaves every step but the first.  d1_w: down1's packed weights (wpack layout, bf16x3 chunk order).
   const void* d1_w;
   const float* d1_tmap;      // [T][24][256] time contribution + biases of level 1
-  const float* d1_cmap;      // [n_tac][24][256] label contribution (condition 0)
+  const float* d1_cmap;      // [n_tac][24][256] label contribution (indexed by next.tac per sample)
   void* d1_s1; void* d1_p1;  // [B][24][256], [B][12][256]
 };
 

@@ -463,6 +463,21 @@ __device__ __forceinline__ i32x4 make_rsrc(const void* base, unsigned bytes) {
   return r;
 }
 
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// LDS-DMA of this wave retired to vmcnt <= N, own LDS reads done, then a bare
+// s_barrier (a __syncthreads() would drain every in-flight DMA: vmcnt(0)).
+template <int N>
+__device__ __forceinline__ void ring_barrier() {
+  if constexpr ((CONV_EXP_MODE & 32) != 0) return;
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // XS = 1: the bf16x3 (fp32-class) network.  An fp32 activation row of C channels is stored as
 // [hi(C) | lo(C)] bf16 (hi = bf16(v), lo = bf16(v - hi)), and every input segment of C channels
 // is walked as 3 x C/KC chunks: (a_hi, w_hi), (a_hi, w_lo), (a_lo, w_hi) -- the same bf16 MFMA
@@ -601,7 +616,28 @@ struct DmaPlan {
 // Fused down1 (FinalArgs::d1_w) tile in the final level's LDS, after the down0 map rows [48][128] f32:
 // A = p0 rows of the tile's samples [4 x 24 + zero row][128] bf16 (272-B rows: a 16-lane group's
 // ds_read_b128 covers all 64 banks), then the level-1 map rows [24][256] f32 (time + label + biases).
-constexpr int kD1Ldb = 272, kD1A = 48 * 128 * 4, kD1Rows = 4 * 24, kD1M = kD1A + (kD1Rows + 1) * kD1Ldb;
+// bf16x3 (XS = 1): a p0 row is [hi(128) | lo(128)] (528-B rows, the same 4-dword bank shift per row).
+// Tiles with more than one condition (per-sample tac): the level-1 map rows of sample s live at
+// d1_map_off(s): sample 0 in the dead down0-map rows [0, kD1A), samples 1..3 after the single-condition
+// maps' place (the final level's map rows behind SMEM0 are dead by then as well).
+// FD1_LDS (the B operands through LDS): the level-1 map rows of a several-condition tile are read from L2
+// in the epilogue instead, and the LDS behind the p0 rows and the map holds a ring of B units.
+#ifndef FD1_LDS
+#define FD1_LDS 1
+#endif
+template <int XS> struct D1L {
+  static constexpr int Ldb = XS ? 528 : 272, A = 48 * 128 * 4, Rows = 4 * 24, M = A + (Rows + 1) * Ldb;
+  static constexpr int MAPB = 24 * 256 * 4;
+  static __device__ __forceinline__ int map_off(bool mixed, int s) { return !mixed ? M : s == 0 ? 0 : M + (s - 1) * MAPB; }
+  // FD1_LDS ring: a B unit = one (chunk, tap) of all 4 N-tiles = 4 x 4 KB; slots from the end of the map
+  // rows to the end of the final level's LDS (bf16x3: 3 there + one in the dead down0-map rows)
+  static constexpr int UNIT = 4 * 4096, SLOT0 = (M + MAPB + 255) / 256 * 256;
+  static constexpr int NS_HI = (162560 - SLOT0) / UNIT;
+  static constexpr int NS = NS_HI >= 5 ? 5 : NS_HI + 1;
+  static_assert(NS * 4096 >= (XS ? 12288 : 18432), "wave-private staging of the s1 / p1 rows");
+  static constexpr __host__ __device__ int slot_off(int s) { return s < NS_HI ? SLOT0 + s * UNIT : 0; }
+};
+constexpr int kD1M = D1L<0>::M;
 
 // Measured (profiles/r02/ab/fused_down1): the first version cost 15-18 us inside up2 against 14.5 us
 // for the standalone down1 launch (1.3 % slower end to end): the compiler had sunk every B load to
@@ -630,25 +666,45 @@ constexpr int kD1Ldb = 272, kD1A = 48 * 128 * 4, kD1Rows = 4 * 24, kD1M = kD1A +
 #ifndef FD1_EARLY
 #define FD1_EARLY 0
 #endif
-// B fragments of iteration it (chunk it / 6 rotated by rot, tap it % 6), both k-groups and N-halves
-template <typename FA>
-__device__ __forceinline__ void fd1_ldb(const FA& f, int w, int lane, int it, int rot, bf16x8 (&dst)[2][2]) {
-  constexpr int NTD = 64, ROWBD = 64, BBYTES = 6 * NTD * ROWBD, TILE = 4 * BBYTES;
+// B fragments of iteration it (chunk it / 6 rotated by rot, tap it % 6), both k-groups and N-halves.
+// bf16x3: 12 chunks in DmaPlan::coff order -- (a_hi, w_hi) x 4, (a_hi, w_lo) x 4, (a_lo, w_hi) x 4.
+template <typename T, int XS, typename FA>
+__device__ __forceinline__ void fd1_ldb(const FA& f, int w, int lane, int it, int rot,
+                                        typename Frag<T>::type (&dst)[2][2]) {
+  typedef typename Frag<T>::type fragT;
+  constexpr int NTD = 64, ROWBD = 64, BBYTES = 6 * NTD * ROWBD, NCH = XS ? 12 : 4, TILE = NCH * BBYTES;
   const int lr = lane & 31, h = lane >> 5;
-  const char* base = reinterpret_cast<const char*>(f.d1_w) + (size_t)w * TILE + (((it / 6) + rot) & 3) * BBYTES +
+  const char* base = reinterpret_cast<const char*>(f.d1_w) + (size_t)w * TILE + (((it / 6) + rot) % NCH) * BBYTES +
                      (it % 6) * NTD * ROWBD;
 #pragma unroll
   for (int g = 0; g < 2; ++g)
 #pragma unroll
     for (int jn = 0; jn < 2; ++jn) {
       const int n = jn * 32 + lr;
-      dst[g][jn] = *reinterpret_cast<const bf16x8*>(base + ((n * ROWBD + ((h ^ ((n >> 2) & 3)) << 4)) ^ (g << 5)));
+      dst[g][jn] = *reinterpret_cast<const fragT*>(base + ((n * ROWBD + ((h ^ ((n >> 2) & 3)) << 4)) ^ (g << 5)));
     }
 }
-template <typename FA>
-__device__ __forceinline__ void fused_down1(const FA& f, char* smem, int m0, int nb, int w, int lane,
-                                            bf16x8 (&bq)[FD1_RING][2][2]) {
+template <typename T> __device__ __forceinline__ T to_t(float v);
+template <> __device__ __forceinline__ bf16 to_t<bf16>(float v) { return (bf16)v; }
+template <> __device__ __forceinline__ f16 to_t<f16>(float v) { return (f16)v; }
+// one activation value into row `row` (channel n) of a C-channel 16-bit tensor (XS: [hi | lo] rows)
+template <typename T, int XS>
+__device__ __forceinline__ void store_scalar(T* base, size_t row, int C, int n, float v) {
+  if constexpr (XS != 0) {
+    const T hi = to_t<T>(v);
+    base[row * 2 * C + n] = hi;
+    base[row * 2 * C + C + n] = to_t<T>(v - (float)hi);
+  } else {
+    base[row * C + n] = to_t<T>(v);
+  }
+}
+template <typename T, int XS, typename FA>
+__device__ __forceinline__ void fused_down1(const FA& f, char* smem, int m0, int nb, int w, int lane, bool mixed,
+                                            typename Frag<T>::type (&bq)[FD1_RING][2][2]) {
+  typedef typename Frag<T>::type fragT;
+  using DL = D1L<XS>;
   constexpr int NTD = 64;   // output channels per wave (down1 N-tile)
+  constexpr int NCH = XS ? 12 : 4, NIT = 6 * NCH, NST = 2 * NIT;
   const int lr = lane & 31, h = lane >> 5;
   int aoff[6][3];
 #pragma unroll
@@ -656,15 +712,16 @@ __device__ __forceinline__ void fused_down1(const FA& f, char* smem, int m0, int
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const int r = i * 32 + lr, sm = r / 24, l = r - 24 * sm, p = l + j - 2;
-      const int row = (p >= 0 && p < 24) ? sm * 24 + p : kD1Rows;
-      aoff[j][i] = kD1A + row * kD1Ldb + h * 16;
+      const int row = (p >= 0 && p < 24) ? sm * 24 + p : DL::Rows;
+      aoff[j][i] = DL::A + row * DL::Ldb + h * 16;
     }
   // FD1_ROT: the chunk order starts at chunk (blockIdx / 8) mod 4, so the 32 workgroups of an XCD
   // do not all stream the same weight lines at once (changes the fp32 accumulation order: not
-  // bitwise equal to the standalone launch)
-  const int rot = FD1_ROT ? (int)((blockIdx.x >> 3) & 3) : 0;
+  // bitwise equal to the standalone launch; bf16 only)
+  const int rot = (FD1_ROT && !XS) ? (int)((blockIdx.x >> 3) & 3) : 0;
   constexpr int RING = FD1_RING;
-  auto ldb = [&](int it, bf16x8 (&dst)[2][2]) { fd1_ldb(f, w, lane, it, rot, dst); };
+  static_assert(24 % RING == 0 || NIT == 24, "register ring index pattern");
+  auto ldb = [&](int it, fragT (&dst)[2][2]) { fd1_ldb<T, XS>(f, w, lane, it, rot, dst); };
   f32x16 acc[3][2];
 #pragma unroll
   for (int i = 0; i < 3; ++i)
@@ -672,27 +729,29 @@ __device__ __forceinline__ void fused_down1(const FA& f, char* smem, int m0, int
     for (int jn = 0; jn < 2; ++jn)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][jn][e] = 0.f;
-  if (!FD1_EARLY || FD1_ROT) {
+  if (!FD1_EARLY || FD1_ROT || XS) {
 #pragma unroll
     for (int it = 0; it < RING - 1; ++it) ldb(it, bq[it]);
   }
-  // A fragments of step st = 2 it + g (chunk kc, tap j, k-group g), read one step ahead
-  auto lda = [&](int st, bf16x8 (&dst)[3]) {
-    const int it = st >> 1, g = st & 1, kc = ((it / 6) + rot) & 3, j = it % 6;
+  // A fragments of step st = 2 it + g (chunk kc, tap j, k-group g), read one step ahead; the chunk's
+  // channel offset is DmaPlan::coff's (bf16x3: chunks 8..11 read the lo half of the row)
+  auto lda = [&](int st, fragT (&dst)[3]) {
+    const int it = st >> 1, g = st & 1, kc = ((it / 6) + rot) % NCH, j = it % 6;
+    const int cb = (kc & 3) * 64 + (XS && kc >= 8 ? 256 : 0);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) dst[i] = *reinterpret_cast<const bf16x8*>(smem + aoff[j][i] + kc * 64 + g * 32);
+    for (int i = 0; i < 3; ++i) dst[i] = *reinterpret_cast<const fragT*>(smem + aoff[j][i] + cb + g * 32);
   };
-  bf16x8 av[2][3];
+  fragT av[2][3];
   lda(0, av[0]);
   // the scheduler would sink each B load to just before its MFMAs (vmcnt(1..3) waits, a
   // latency-bound stream) and each A read likewise; the barriers keep the B ring RING - 1
   // iterations and the A reads one step ahead
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int st = 0; st < 48; ++st) {              // (chunk kc, tap j) = ((it / 6 + rot) mod 4, it % 6)
+  for (int st = 0; st < NST; ++st) {             // (chunk kc, tap j) = ((it / 6 + rot) mod NCH, it % 6)
     const int it = st >> 1, g = st & 1;
-    if (g == 0 && it + RING - 1 < 24) ldb(it + RING - 1, bq[(it + RING - 1) % RING]);
-    if (st + 1 < 48) lda(st + 1, av[(st + 1) & 1]);
+    if (g == 0 && it + RING - 1 < NIT) ldb(it + RING - 1, bq[(it + RING - 1) % RING]);
+    if (st + 1 < NST) lda(st + 1, av[(st + 1) & 1]);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < 3; ++i)
@@ -703,15 +762,15 @@ __device__ __forceinline__ void fused_down1(const FA& f, char* smem, int m0, int
       }
     __builtin_amdgcn_sched_barrier(0);
   }
-  // epilogue: accumulator rows (e, e + 1) are positions (l, l + 1) of one sample.  The pooled p1
-  // goes out from registers (2-B stores); the s1 rows (FD1_STAGE) are staged as bf16 in this wave's
+  // epilogue: accumulator rows (e, e + 1) are positions (l, l + 1) of one sample.  s1 and the pooled p1
+  // go out from registers (2-B stores); the s1 rows (FD1_STAGE, bf16 only) are staged in this wave's
   // [96][64] slice of the dead down0-map / A-tile region and leave as 16-B stores of 8 channels
-  const float* md = reinterpret_cast<const float*>(smem + kD1M);
-  bf16* s1 = reinterpret_cast<bf16*>(f.d1_s1);
-  bf16* p1 = reinterpret_cast<bf16*>(f.d1_p1);
+  T* s1 = reinterpret_cast<T*>(f.d1_s1);
+  T* p1 = reinterpret_cast<T*>(f.d1_p1);
+  constexpr bool STAGE = FD1_STAGE && !XS && std::is_same<T, bf16>::value;
   bf16* stg = reinterpret_cast<bf16*>(smem) + w * 96 * NTD;      // 12 KB per wave, below kD1M
   static_assert(4 * 96 * NTD * 2 <= kD1M, "s1 staging stays below the level-1 map rows");
-  if (FD1_STAGE) __syncthreads();                // every wave is done with the A tile
+  if (STAGE) __syncthreads();                    // every wave is done with the A tile
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -721,27 +780,28 @@ __device__ __forceinline__ void fused_down1(const FA& f, char* smem, int m0, int
       for (int e = 0; e < 16; e += 2) {
         const int r = i * 32 + 8 * (e >> 2) + 4 * h + (e & 3);
         const int sm = r / 24, l = r - 24 * sm;
+        const float* md = reinterpret_cast<const float*>(smem + DL::map_off(mixed, sm));
         const float v0 = fmaxf(acc[i][jn][e] + md[l * 256 + n], 0.f);
         const float v1 = fmaxf(acc[i][jn][e + 1] + md[(l + 1) * 256 + n], 0.f);
-        if (FD1_STAGE) {
+        if (STAGE) {
           stg[r * NTD + jn * 32 + lr] = (bf16)v0;
           stg[(r + 1) * NTD + jn * 32 + lr] = (bf16)v1;
         }
         if (sm < nb) {
           const size_t row = (size_t)(m0 + sm) * 24 + l;
           if constexpr (FD1_DIAG == 1) {
-            if (v0 == 12345.f && v1 == 54321.f) s1[row * 256 + n] = (bf16)v0;
+            if (v0 == 12345.f && v1 == 54321.f) s1[row * 256 + n] = (T)v0;
             continue;
           }
-          if (!FD1_STAGE) {
-            s1[row * 256 + n] = (bf16)v0;
-            s1[(row + 1) * 256 + n] = (bf16)v1;
+          if (!STAGE) {
+            store_scalar<T, XS>(s1, row, 256, n, v0);
+            store_scalar<T, XS>(s1, row + 1, 256, n, v1);
           }
-          p1[((size_t)(m0 + sm) * 12 + (l >> 1)) * 256 + n] = (bf16)fmaxf(v0, v1);
+          store_scalar<T, XS>(p1, (size_t)(m0 + sm) * 12 + (l >> 1), 256, n, fmaxf(v0, v1));
         }
       }
     }
-  if (FD1_STAGE && FD1_DIAG != 1) {
+  if (STAGE && FD1_DIAG != 1) {
     __syncthreads();                             // (the staging slices are per wave; one barrier)
 #pragma unroll
     for (int q = 0; q < 12; ++q) {               // 96 rows x 8 pieces of 16 B per wave
@@ -749,7 +809,7 @@ __device__ __forceinline__ void fused_down1(const FA& f, char* smem, int m0, int
       const int sm = r / 24, l = r - 24 * sm;
       if (sm < nb) {
         const bf16x8 v = *reinterpret_cast<const bf16x8*>(stg + r * NTD + c8);
-        *reinterpret_cast<bf16x8*>(s1 + ((size_t)(m0 + sm) * 24 + l) * 256 + w * NTD + c8) = v;
+        *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(s1) + ((size_t)(m0 + sm) * 24 + l) * 256 + w * NTD + c8) = v;
       }
     }
   }
@@ -828,6 +888,183 @@ __device__ __forceinline__ void store_act(T* base, size_t row, int C, int n, con
   else Vec8<T>::store(base + row * C + n, v);
 }
 
+// Fused down1 with its B operands staged through LDS (FD1_LDS): the register stream above reads the
+// 393 KB of down1 weights per workgroup (each of the 4 waves its own N-tile, 4 KB per (chunk, tap)
+// unit) at about 33 GB/s per CU.  Here every wave copies its own 4 KB of unit u + D into a ring slot by
+// LDS-DMA (buffer_load ... lds, 4 instructions per lane, a fixed count per unit so every vmcnt wait is
+// one constant; the units past the last are out-of-range reads that land zeros in dead slots), reads
+// unit u + 1's B fragments from LDS while the MFMAs of unit u run, and the A fragments one step ahead as
+// above.  One s_barrier per unit (the waves' slot writes and reads), the same operands and accumulation
+// order: bitwise equal to the standalone conv_kernel<down1>.
+template <typename T, int XS, bool MIXED, typename FA>
+__device__ __forceinline__ void fused_down1_lds(const FA& f, char* smem, int m0, int nb, int w, int lane, int t_next,
+                                                const int* tac_next, int B) {
+  typedef typename Frag<T>::type fragT;
+  using DL = D1L<XS>;
+  constexpr int NTD = 64, NCH = XS ? 12 : 4, NU = 6 * NCH, NS = DL::NS, D = NS - 1;
+  static_assert(NS >= 3 && D - 2 >= 0 && 4 * (D - 2) < 64, "ring depth");
+  const int lr = lane & 31, h = lane >> 5;
+  int aoff[6][3];
+#pragma unroll
+  for (int j = 0; j < 6; ++j)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int r = i * 32 + lr, sm = r / 24, l = r - 24 * sm, p = l + j - 2;
+      const int row = (p >= 0 && p < 24) ? sm * 24 + p : DL::Rows;
+      aoff[j][i] = DL::A + row * DL::Ldb + h * 16;
+    }
+  int boff[2][2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int jn = 0; jn < 2; ++jn) {
+      const int n = jn * 32 + lr;
+      boff[g][jn] = w * 4096 + ((n * 64 + ((h ^ ((n >> 2) & 3)) << 4)) ^ (g << 5));
+    }
+  constexpr int TILE = NCH * 6 * 4096;
+  const i32x4 rsw = make_rsrc(f.d1_w, 4u * (unsigned)TILE);
+  // unit u of this wave: its 4 KB at w * TILE + u * 4096 (chunk u / 6, tap u % 6 are consecutive)
+  auto issue = [&](int u) {
+    char* dst = smem + DL::slot_off(u % NS) + w * 4096;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int off = u < NU ? w * TILE + u * 4096 + k * 1024 + lane * 16 : 0x7ffffff0;   // past the end: zeros
+      llvm_amdgcn_raw_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(dst + k * 1024), 16, off, 0, 0, 0);
+    }
+  };
+  f32x16 acc[3][2];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][jn][e] = 0.f;
+#pragma unroll
+  for (int u = 0; u < D; ++u) issue(u);
+  auto ldb = [&](int u, fragT (&dst)[2][2]) {
+    const char* base = smem + DL::slot_off(u % NS);
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn) dst[g][jn] = *reinterpret_cast<const fragT*>(base + boff[g][jn]);
+  };
+  auto lda = [&](int st, fragT (&dst)[3]) {
+    const int u = st >> 1, g = st & 1, kc = u / 6, j = u % 6;
+    const int cb = (kc & 3) * 64 + (XS && kc >= 8 ? 256 : 0);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) dst[i] = *reinterpret_cast<const fragT*>(smem + aoff[j][i] + cb + g * 32);
+  };
+  fragT bv[2][2][2], av[2][3];
+  wait_vmcnt<4 * (D - 1)>();                     // unit 0 landed (own DMA)
+  ring_barrier<4 * (D - 1)>();                   // ... for every wave
+  ldb(0, bv[0]);
+  lda(0, av[0]);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    // unit u + 1 landed for every wave; every wave is done reading slot (u - 1) % NS = (u + D) % NS
+    ring_barrier<4 * (D - 2)>();
+    issue(u + D);
+    if (u + 1 < NU) ldb(u + 1, bv[(u + 1) & 1]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int st = 2 * u + g;
+      if (st + 1 < 2 * NU) lda(st + 1, av[(st + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int jn = 0; jn < 2; ++jn) acc[i][jn] = mfma32(av[st & 1][i], bv[u & 1][g][jn], acc[i][jn]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  wait_vmcnt<0>();                               // the dummy units are out of the LDS before it is reused
+  T* s1 = reinterpret_cast<T*>(f.d1_s1);
+  T* p1 = reinterpret_cast<T*>(f.d1_p1);
+  const float* tm1 = f.d1_tmap + (size_t)t_next * 24 * 256;
+  // relu(acc + maps) in place: accumulator rows (e, e + 1) are positions (l, l + 1) of one sample
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int jn = 0; jn < 2; ++jn) {
+      const int n = w * NTD + jn * 32 + lr;
+#pragma unroll
+      for (int e = 0; e < 16; e += 2) {
+        const int r = i * 32 + 8 * (e >> 2) + 4 * h + (e & 3);
+        const int sm = r / 24, l = r - 24 * sm;
+        float m0v, m1v;
+        if constexpr (MIXED) {   // time + this sample's label rows from L2 (tmap + cmap, the standalone order)
+          const int tac_s = tac_next ? tac_next[min(m0 + sm, B - 1)] : 0;
+          const float* cm1 = f.d1_cmap + (size_t)tac_s * 24 * 256;
+          m0v = tm1[l * 256 + n] + cm1[l * 256 + n];
+          m1v = tm1[(l + 1) * 256 + n] + cm1[(l + 1) * 256 + n];
+        } else {
+          const float* md = reinterpret_cast<const float*>(smem + DL::M);
+          m0v = md[l * 256 + n];
+          m1v = md[(l + 1) * 256 + n];
+        }
+        acc[i][jn][e] = fmaxf(acc[i][jn][e] + m0v, 0.f);
+        acc[i][jn][e + 1] = fmaxf(acc[i][jn][e + 1] + m1v, 0.f);
+      }
+    }
+  // The s1 / p1 rows leave as 16-B stores of 8 channels (one 2-B store per value and lane had kept the
+  // fused down1 at ~12 us, most of it draining 73 KB per workgroup of 2-B writes): each wave stages its
+  // [96][64] s1 and [48][64] pooled p1 slices as 16-bit rows in its OWN 4-KB parts of the ring slots
+  // (written only by this wave's DMAs, all landed: no barrier), then reads back 16-B pieces.
+  // bf16x3 rows are [hi(256) | lo(256)]: one plane per round (16 KB of private staging).
+  auto stg = [&](int q) -> char* { return smem + DL::slot_off(q >> 12) + w * 4096 + (q & 4095); };
+  auto put = [&](int q, float v, int pl) {
+    const T hi = to_t<T>(v);
+    *reinterpret_cast<T*>(stg(q)) = pl ? to_t<T>(v - (float)hi) : hi;
+  };
+  auto put_s1 = [&](int pl) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) put((i * 32 + 8 * (e >> 2) + 4 * h + (e & 3)) * 128 + (jn * 32 + lr) * 2,
+                                         acc[i][jn][e], pl);
+  };
+  auto put_p1 = [&](int q0, int pl) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+        for (int e = 0; e < 16; e += 2)
+          put(q0 + ((i * 32 + 8 * (e >> 2) + 4 * h + (e & 3)) >> 1) * 128 + (jn * 32 + lr) * 2,
+              fmaxf(acc[i][jn][e], acc[i][jn][e + 1]), pl);
+  };
+  // rows [0, nrows) of 128 B at staging offset q0 -> global rows of tensor `base` (L positions per sample)
+  auto flush = [&](T* base, int nrows, int L_, int q0, int pl) {
+    for (int k = 0; k < nrows / 8; ++k) {
+      const int pc = k * 64 + lane, r = pc >> 3, c = pc & 7, sm = r / L_, l = r - sm * L_;
+      if (sm < nb) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(stg(q0 + r * 128 + c * 16));
+        T* dst = base + ((size_t)(m0 + sm) * L_ + l) * (XS ? 512 : 256) + pl * 256 + w * NTD + c * 8;
+        store16(reinterpret_cast<bf16x8*>(dst), v);
+      }
+    }
+  };
+  if constexpr (XS == 0) {
+    put_s1(0);
+    put_p1(96 * 128, 0);
+    flush(s1, 96, 24, 0, 0);
+    flush(p1, 48, 12, 96 * 128, 0);
+  } else {
+    put_s1(0);
+    flush(s1, 96, 24, 0, 0);
+    put_s1(1);
+    flush(s1, 96, 24, 0, 1);
+    put_p1(0, 0);
+    put_p1(48 * 128, 1);
+    flush(p1, 48, 12, 0, 0);
+    flush(p1, 48, 12, 48 * 128, 1);
+  }
+}
+
 // down0 positions pos0, pos0 + pstride, ... of samples b0 .. b0 + nb - 1: x from LDS
 // (xs [nb][96]), maps from LDS (mp [48][128], fast) or global, weights in registers.
 template <typename T, int XS = 0>
@@ -884,30 +1121,20 @@ __device__ __forceinline__ void down0_positions(const Down0Args& a, const float*
     // p0 feeds only down1: with the fused down1 (p0l) it stays in LDS, no global copy
     if constexpr (!(FIN_EXP & 2)) { if (!p0l) store_act<T, XS>(reinterpret_cast<T*>(a.p0), (size_t)b * 24 + lp, 128, n0, pv); }
     else if (pv[0] == 12345.f) reinterpret_cast<T*>(a.p0)[0] = (T)0.f;
-    if constexpr (sizeof(T) == 2 && XS == 0) {
-      if (p0l) {   // fused down1: the same bf16 row, LDS row bl * 24 + lp (kD1Ldb bytes per row)
-        typename Frag<T>::type o;
+    if constexpr (sizeof(T) == 2) {
+      if (p0l) {   // fused down1: the same 16-bit row, LDS row bl * 24 + lp (D1L<XS>::Ldb bytes per row)
+        typename Frag<T>::type o, r;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) o[q] = (T)pv[q];
-        *reinterpret_cast<typename Frag<T>::type*>(p0l + (bl * 24 + lp) * kD1Ldb + n0 * 2) = o;
+        for (int q = 0; q < 8; ++q) {
+          o[q] = (T)pv[q];
+          r[q] = (T)(pv[q] - (float)o[q]);      // bf16x3: the lo half (Vec8::store_split)
+        }
+        char* row = p0l + (bl * 24 + lp) * D1L<XS>::Ldb;
+        *reinterpret_cast<typename Frag<T>::type*>(row + n0 * 2) = o;
+        if constexpr (XS != 0) *reinterpret_cast<typename Frag<T>::type*>(row + (128 + n0) * 2) = r;
       }
     }
   }
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// LDS-DMA of this wave retired to vmcnt <= N, own LDS reads done, then a bare
-// s_barrier (a __syncthreads() would drain every in-flight DMA: vmcnt(0)).
-template <int N>
-__device__ __forceinline__ void ring_barrier() {
-  if constexpr ((CONV_EXP_MODE & 32) != 0) return;
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
 }
 
 template <typename T, int KIND, int XS = 0>
@@ -2085,35 +2312,73 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
 #pragma unroll
         for (int k = 0; k < 6; ++k) reinterpret_cast<f32x4*>(mp)[tid + kThreads * k] = mv[k];
       }
-      // fused down1 (one condition, bf16): level-1 map rows loaded now, written to LDS after down0
-      constexpr bool D1 = std::is_same<T, bf16>::value && XS == 0 && G::FIN_MAPS;
-      const bool fuse_d1 = D1 && f.d1_w != nullptr && fast;
-      static_assert(!D1 || kD1M + 24 * 256 * 4 <= G::MT * G::FIN_LD * 4, "fused down1 tiles fit the dead C tile");
+      // fused down1 of the next step (16-bit networks: bf16, fp16, bf16x3): level-1 map rows loaded now,
+      // written to LDS after down0.  A tile with more than one condition (per-sample tac) gets one map
+      // per sample, read after down0 (rare: TAC-major batches change condition at tile boundaries)
+      using DL = D1L<XS>;
+      constexpr bool D1 = sizeof(T) == 2 && G::FIN_MAPS;
+      const bool fuse_d1 = D1 && f.d1_w != nullptr;
+      const bool d1_mixed = fuse_d1 && !fast;
+      static_assert(!D1 || DL::M + DL::MAPB <= G::MT * G::FIN_LD * 4, "fused down1 tiles fit the dead C tile");
+      static_assert(!D1 || FD1_LDS || DL::M + 3 * DL::MAPB <= G::SMEM, "per-sample level-1 maps fit the dead LDS");
+      static_assert(!D1 || !FD1_LDS || (G::SMEM == 162560 && DL::slot_off(DL::NS_HI - 1) + DL::UNIT <= G::SMEM &&
+                                        (DL::NS_HI >= DL::NS || DL::UNIT <= DL::A)), "fused down1 B ring fits the LDS");
       static_assert(!D1 || G::MT / L == 4, "fused down1: 4 samples per tile");
       f32x4 m1v[6];
-      bf16x8 bqd[FD1_RING][2][2];
+      typename Frag<T>::type bqd[FD1_RING][2][2];
       if (fuse_d1) {
-        if (FD1_EARLY && !FD1_ROT) {
+        if (FD1_EARLY && !FD1_ROT && !XS && !FD1_LDS) {
 #pragma unroll
-          for (int it = 0; it < FD1_RING - 1; ++it) fd1_ldb(f, wv, lane, it, 0, bqd[it]);
+          for (int it = 0; it < FD1_RING - 1; ++it) fd1_ldb<T, XS>(f, wv, lane, it, 0, bqd[it]);
         }
-        const f32x4* tm1 = reinterpret_cast<const f32x4*>(f.d1_tmap + (size_t)nd.t_uniform * 24 * 256);
-        const f32x4* cm1 = reinterpret_cast<const f32x4*>(f.d1_cmap);
+        if (!d1_mixed) {
+          const int tac_d1 = nd.tac ? nd.tac[m0] : 0;
+          const f32x4* tm1 = reinterpret_cast<const f32x4*>(f.d1_tmap + (size_t)nd.t_uniform * 24 * 256);
+          const f32x4* cm1 = reinterpret_cast<const f32x4*>(f.d1_cmap + (size_t)tac_d1 * 24 * 256);
 #pragma unroll
-        for (int k = 0; k < 6; ++k) m1v[k] = tm1[tid + kThreads * k] + cm1[tid + kThreads * k];
+          for (int k = 0; k < 6; ++k) m1v[k] = tm1[tid + kThreads * k] + cm1[tid + kThreads * k];
+        }
         // zero row + the rows of absent samples (their outputs are not stored; keep them finite)
-        for (int q = tid; q < (kD1Rows + 1 - nb_next * 24) * (kD1Ldb / 16); q += kThreads)
-          *reinterpret_cast<uint4*>(smem + kD1A + nb_next * 24 * kD1Ldb + q * 16) = make_uint4(0, 0, 0, 0);
+        for (int q = tid; q < (DL::Rows + 1 - nb_next * 24) * (DL::Ldb / 16); q += kThreads)
+          *reinterpret_cast<uint4*>(smem + DL::A + nb_next * 24 * DL::Ldb + q * 16) = make_uint4(0, 0, 0, 0);
       }
       __syncthreads();
       if constexpr (!(FIN_EXP & 1)) down0_positions<T, XS>(nd, xst, mp, fast, m0, nb_next, wr, n0_next, tid >> 4, kThreads / 16,
-                                                           fuse_d1 ? smem + kD1A : nullptr);
-      if constexpr (D1) {
+                                                           fuse_d1 ? smem + DL::A : nullptr);
+      if constexpr (D1 && FD1_LDS) {
         if (fuse_d1) {
+          if (!d1_mixed) {
 #pragma unroll
-          for (int k = 0; k < 6; ++k) reinterpret_cast<f32x4*>(smem + kD1M)[tid + kThreads * k] = m1v[k];
+            for (int k = 0; k < 6; ++k) reinterpret_cast<f32x4*>(smem + DL::M)[tid + kThreads * k] = m1v[k];
+          }
+          __syncthreads();                             // p0 rows (and the level-1 maps) in LDS; down0 done
+#if CONV_EXP_MODE & 128
+          if (tid == 0) reinterpret_cast<unsigned long long*>(a.fin.x_all)[6144 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
+          if (d1_mixed) fused_down1_lds<T, XS, true>(f, smem, m0, nb_next, wv, lane, nd.t_uniform, nd.tac, B);
+          else fused_down1_lds<T, XS, false>(f, smem, m0, nb_next, wv, lane, nd.t_uniform, nd.tac, B);
+        }
+      } else if constexpr (D1) {
+        if (fuse_d1) {
+          if (!d1_mixed) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) reinterpret_cast<f32x4*>(smem + DL::M)[tid + kThreads * k] = m1v[k];
+          } else {
+            __syncthreads();                           // every wave is done with the down0 map rows
+            const f32x4* tm1 = reinterpret_cast<const f32x4*>(f.d1_tmap + (size_t)nd.t_uniform * 24 * 256);
+            for (int sm = 0; sm < 4; ++sm) {
+              const int tac_s = nd.tac ? nd.tac[min(m0 + sm, B - 1)] : 0;
+              const f32x4* cm1 = reinterpret_cast<const f32x4*>(f.d1_cmap + (size_t)tac_s * 24 * 256);
+              f32x4* dst = reinterpret_cast<f32x4*>(smem + DL::map_off(true, sm));
+#pragma unroll
+              for (int k = 0; k < 6; ++k) dst[tid + kThreads * k] = tm1[tid + kThreads * k] + cm1[tid + kThreads * k];
+            }
+          }
           __syncthreads();                             // p0 rows and level-1 maps in LDS
-          fused_down1(f, smem, m0, nb_next, wv, lane, bqd);
+#if CONV_EXP_MODE & 128
+          if (tid == 0) reinterpret_cast<unsigned long long*>(a.fin.x_all)[6144 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
+          fused_down1<T, XS>(f, smem, m0, nb_next, wv, lane, d1_mixed, bqd);
         }
       }
 #if CONV_EXP_MODE & 128

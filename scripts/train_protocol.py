@@ -148,6 +148,9 @@ def main():
         torch.cuda.synchronize()
         rec['mcmc_seconds'] = round(time.perf_counter() - t0, 3)
         rec['mcmc_accept_rate'] = round(float(res['accept_rate'].mean()), 4)
+        conv = res['convergence']                       # mcmc.py:183-194
+        rec['mcmc_rhat_max'] = round(conv['rhat_max'], 5)
+        rec['mcmc_rhat_flag_gt_1.02'] = conv['flag']
         draws = res['draws']
         for tag, dt in samplers:
             m = ImprovedDDPM(network=net, dtype=dt, **shipped_diff_args())

@@ -359,24 +359,31 @@ def test_fused_next_step_down0_bitwise(conds, dtype, monkeypatch):
     fused.close()
 
 
-def test_fused_next_step_down1_bitwise(conds, monkeypatch):
+@pytest.mark.parametrize('dtype', ['bfloat16', 'float16', 'bf16x3'])
+def test_fused_next_step_down1_bitwise(conds, dtype, monkeypatch):
     """PETDIFF_FUSE_DOWN1=1 also runs step i+1's down1 (Conv1D 128 -> 256 + MaxPool) inside step i's
-    final epilogue, on the tile's own p0 rows (bf16, one condition; on by default,
-    PETDIFF_FUSE_DOWN1=0 keeps the standalone launch).  Same operands and fp32 MFMA accumulation order as the standalone conv_kernel<down1>:
-    bit-identical samples, ragged batch (an incomplete last tile), graph and eager."""
+    final epilogue, on the tile's own p0 rows (the 16-bit networks: bf16, fp16 and bf16x3's 12 hi/lo
+    chunks; on by default, PETDIFF_FUSE_DOWN1=0 keeps the standalone launch).  Same operands and fp32
+    MFMA accumulation order as the standalone conv_kernel<down1>: bit-identical samples, ragged batch (an
+    incomplete last tile), graph and eager, one condition (the LDS map path) and conditions interleaved
+    per sample (tiles with several conditions: per-sample level-1 maps)."""
     rng = np.random.default_rng(25)
     B = 37
     x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    table = np.stack([conds[0], conds[1], conds[0] * 0.9 + 0.05])
+    tac = rng.integers(0, 3, B).astype(np.int32)
     monkeypatch.setenv('PETDIFF_FUSE_DOWN1', '0')
-    plain = make_model('bfloat16')
+    plain = make_model(dtype)
     plain._ensure_handle()
     monkeypatch.setenv('PETDIFF_FUSE_DOWN1', '1')
-    fused = make_model('bfloat16')
+    fused = make_model(dtype)
     fused._ensure_handle()
-    for g in (True, False):
-        a = plain.ddpm_loop(x, conds[:1], num_timesteps=25, seed=4, use_graph=g)
-        b = fused.ddpm_loop(x, conds[:1], num_timesteps=25, seed=4, use_graph=g)
-        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    for kw in ({'tac': tac}, {}):
+        cset = table if kw else conds[:1]
+        for g in (True, False):
+            a = plain.ddpm_loop(x, cset, num_timesteps=25, seed=4, use_graph=g, **kw)
+            b = fused.ddpm_loop(x, cset, num_timesteps=25, seed=4, use_graph=g, **kw)
+            torch.testing.assert_close(a, b, rtol=0, atol=0)
     plain.close()
     fused.close()
 
