@@ -152,9 +152,10 @@ struct petdiff_ctx {
   // run the next step's down0 inside the previous step's up2.block epilogue (generate);
   // PETDIFF_FUSE_DOWN0=0 restores the standalone down0 launch per step (A/B switch)
   bool fuse_down0 = true;
-  // ... and the next step's down1 too (16-bit networks; PETDIFF_FUSE_DOWN1=0: standalone launch).
-  // Bitwise equal; bf16: +0.3..0.8 % end to end in three A/B calls (unet_kernels.hip, fused_down1)
-  bool fuse_down1 = true;
+  // ... and the next step's down1 too (16-bit networks; PETDIFF_FUSE_DOWN1=1).  Bitwise equal; measured a
+  // wash against the standalone launch in round 3 (bf16 -0.1..-0.6 %, bf16x3 0..+0.6 %, fp16 -0.5..+0.1 %,
+  // in-process A/B, profiles/r03/fused_down1), so off by default
+  bool fuse_down1 = false;
   DevBuf xa, xb, tacbuf, tbuf, rng;
   hipStream_t cap_stream = nullptr;
   hipStream_t split_stream = nullptr;  // second launch stream of a split generate (PETDIFF_SPLIT)

@@ -173,8 +173,15 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
         dz.push_back((d6[b] - e2[2 * b + 1]) * 0.01);
         dd.push_back((t4[4 * b + 3] - d6[b]) * 0.01);
       }
-      printf("   final epilogue us: staging %.2f | row loop %.2f | down0 + maps %.2f | fused down1 %.2f (max %.2f)\n",
-             med(ea), med(eb), med(dz), med(dd), mx(dd));
+      std::vector<unsigned long long> d7(nb);
+      CK(hipMemcpy(d7.data(), dbg + 7168, nb * 8, hipMemcpyDeviceToHost));
+      std::vector<double> dk, de;
+      for (int b = 0; b < nb; ++b) {
+        dk.push_back(d7[b] ? (d7[b] - d6[b]) * 0.01 : 0.0);
+        de.push_back(d7[b] ? (t4[4 * b + 3] - d7[b]) * 0.01 : 0.0);
+      }
+      printf("   final epilogue us: staging %.2f | row loop %.2f | down0 + maps %.2f | fused down1 %.2f (max %.2f)"
+             " = K loop %.2f + epilogue and drain %.2f\n", med(ea), med(eb), med(dz), med(dd), mx(dd), med(dk), med(de));
     }
     printf("   loop cycles median %.0f (%.1f per MFMA), clock median %.3f GHz [%.3f..%.3f]\n", cyc[nb / 2],
            cyc[nb / 2] / nmfma, clk[nb / 2], clk[0], clk[nb - 1]);

@@ -363,7 +363,7 @@ def test_fused_next_step_down0_bitwise(conds, dtype, monkeypatch):
 def test_fused_next_step_down1_bitwise(conds, dtype, monkeypatch):
     """PETDIFF_FUSE_DOWN1=1 also runs step i+1's down1 (Conv1D 128 -> 256 + MaxPool) inside step i's
     final epilogue, on the tile's own p0 rows (the 16-bit networks: bf16, fp16 and bf16x3's 12 hi/lo
-    chunks; on by default, PETDIFF_FUSE_DOWN1=0 keeps the standalone launch).  Same operands and fp32
+    chunks; off by default since round 3 -- a wash against the standalone launch -- PETDIFF_FUSE_DOWN1=1).  Same operands and fp32
     MFMA accumulation order as the standalone conv_kernel<down1>: bit-identical samples, ragged batch (an
     incomplete last tile), graph and eager, one condition (the LDS map path) and conditions interleaved
     per sample (tiles with several conditions: per-sample level-1 maps)."""
