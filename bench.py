@@ -320,7 +320,7 @@ def main_mh(args):
             'metric': 'MH chain-steps/sec (48-ROI SRTM2, element-wise Metropolis)', 'value': round(value, 1),
             'unit': 'chain-steps/s', 'n_gpus': world, 'steps': 1, 'warmup': 1,
             'ms_per_step': round(elapsed * 1e3, 3), 'higher_is_better': True, 'scaling': 'weak',
-            'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic (SRTM2 TAC + noise model, synthetic priors)',
+            'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic (SRTM2 TAC + noise model, reference prior prior_stats_nROI48)',
             'config': {'workload': 'mcmc.py Metropolis-Hastings, 48 ROI x 2 params, SRTM2', 'chains_per_gpu': n,
                        'steps_per_chain': iters + tune, 'tune': tune},
             'roofline': {'bound': 'valu-fp64', 'achieved': round(flops, 2), 'peak': 78.6, 'unit': 'TFLOP/s',
@@ -425,7 +425,7 @@ def main_train(args):
             'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': 'f32',
-            'data': 'synthetic (GPU SRTM2 generator: truncated-MVN priors + noise model; Glorot init)',
+            'data': 'synthetic (GPU SRTM2 generator: truncated-MVN reference prior + noise model; Glorot init)',
             'config': {'workload': 'iDDPM training step (q-sample, U-Net fwd/bwd, MSE + 0.1 VLB, clipped Adam)',
                        'batch_per_gpu': B, 'global_batch': world * B,
                        'parallelism': f'dp{world} (RCCL all-reduce of the fp32 gradient blob)'},
@@ -691,7 +691,8 @@ def main():
             'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': {'bfloat16': 'bf16', 'float16': 'f16', 'float32': 'f32',
                                                     'bf16x3': 'bf16x3 (fp32-class)'}[args.dtype],
-            'data': 'synthetic (SRTM2 TACs + noise model; identity-denoiser Glorot weights of the shipped net)',
+            'data': 'synthetic (test TACs drawn from the reference prior prior_stats_nROI48 + SRTM2 + noise model; '
+                    'identity-denoiser Glorot weights of the shipped net)',
             'config': {'workload': 'iDDPM reverse process, f128/d4 1-D conditional U-Net, 48-ROI x 2 params',
                        'n_posterior_per_gpu': B, 'reverse_steps': n_rev, 'global_batch': world * B,
                        'tacs': world * n_tac, 'samples_per_launch': min(B, chunk),

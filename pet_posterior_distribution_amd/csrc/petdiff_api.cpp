@@ -156,6 +156,10 @@ struct petdiff_ctx {
   // wash against the standalone launch in round 3 (bf16 -0.1..-0.6 %, bf16x3 0..+0.6 %, fp16 -0.5..+0.1 %,
   // in-process A/B, profiles/r03/fused_down1), so off by default
   bool fuse_down1 = false;
+  // down2 -> down3 in one launch with per-sample-block hand-off counters (PETDIFF_SEAM23=1, 16-bit
+  // networks; an experiment); seam: its counters (zeroed once, reset by each launch)
+  bool seam23 = false;
+  DevBuf seam;
   DevBuf xa, xb, tacbuf, tbuf, rng;
   hipStream_t cap_stream = nullptr;
   hipStream_t split_stream = nullptr;  // second launch stream of a split generate (PETDIFF_SPLIT)
@@ -366,6 +370,8 @@ int ensure_workspace(petdiff_ctx* h, int B) {
   HIPC(h->tacbuf.alloc(Bz * 4));
   HIPC(h->tbuf.alloc(Bz * 4));
   HIPC(h->rng.alloc(16 * kMaxSplit));
+  HIPC(h->seam.alloc(((size_t)(B + 63) / 64 + 2) * 4));
+  HIPC(hipMemset(h->seam.p, 0, ((size_t)(B + 63) / 64 + 2) * 4));
   // workspace moved: cached graphs hold stale pointers
   for (auto& kv : h->graphs) {
     if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
@@ -514,6 +520,33 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
       continue;
     }
     if (li == LK_DOWN1 && d1_fuse && io.skip_down0) continue;   // done by the previous step's epilogue
+    auto conv_args = [&](int lj) {
+      const ConvLayer& c = kConv[lj];
+      ConvArgs<T> x{};
+      x.src1 = reinterpret_cast<const T*>(lio[lj].s1);
+      x.c1 = lio[lj].c1;
+      x.src2 = reinterpret_cast<const T*>(lio[lj].s2);
+      x.c2 = lio[lj].c2;
+      x.wpack = h->wpack[lj].as<T>();
+      x.out = reinterpret_cast<T*>(lio[lj].out);
+      x.out_pool = reinterpret_cast<T*>(lio[lj].pool);
+      x.cmap = h->cmap[c.cond_level].as<float>();
+      x.tmap = h->tmap[c.cond_level].as<float>();
+      x.tac = io.tac;
+      x.tvec = io.tvec;
+      x.t_uniform = io.t_uniform;
+      x.n_t = h->T;
+      x.n_tac = h->n_tac;
+      x.B = B;
+      x.cout = c.cout;
+      return x;
+    };
+    if (li == LK_DOWN2 && h->seam23 && sizeof(T) == 2) {     // down2 + down3 in one launch
+      const ConvArgs<T> a2 = conv_args(LK_DOWN2), a3 = conv_args(LK_DOWN3);
+      CHK(timed(1 + li, [&] { return launch_seam23<T>(a2, a3, h->seam.as<int>(), s, h->x3); }));
+      ++li;                                                      // down3 ran in the same launch
+      continue;
+    }
     ConvArgs<T> a{};
     a.src1 = reinterpret_cast<const T*>(lio[li].s1);
     a.c1 = lio[li].c1;
@@ -651,6 +684,7 @@ int petdiff_create(const petdiff_config* cfg, const float* weights, size_t n_wei
   h->spec = make_spec(*cfg, h->n_out);
   if (const char* e = std::getenv("PETDIFF_FUSE_DOWN0")) h->fuse_down0 = std::atoi(e) != 0;
   if (const char* e = std::getenv("PETDIFF_FUSE_DOWN1")) h->fuse_down1 = std::atoi(e) != 0;
+  if (const char* e = std::getenv("PETDIFF_SEAM23")) h->seam23 = std::atoi(e) != 0 && cfg->dtype != PETDIFF_DTYPE_F32;
   h->fuse_up = cfg->dtype != PETDIFF_DTYPE_F32;
   if (const char* e = std::getenv("PETDIFF_FUSE_UP")) h->fuse_up = h->fuse_up && std::atoi(e) != 0;
   const size_t need = h->spec.back().off + h->spec.back().size;

@@ -96,6 +96,10 @@ struct ConvArgs {
 // x3: the bf16x3 network (T = bf16 only; activations stored as [hi | lo] rows, see DmaPlan)
 template <typename T>
 hipError_t launch_conv(int layer_kind, const ConvArgs<T>& a, hipStream_t s, bool x3 = false);
+// down2 and down3 in one launch with per-sample-block hand-off counters (PETDIFF_SEAM23 experiment);
+// seam_state: device int [ceil(B / 64) + 2], zero before the first launch, left zero by each launch
+template <typename T>
+hipError_t launch_seam23(const ConvArgs<T>& a2, const ConvArgs<T>& a3, int* seam_state, hipStream_t s, bool x3 = false);
 template <typename T>
 hipError_t launch_down0(const Down0Args& a, hipStream_t s, bool x3 = false);
 hipError_t launch_split_to_f32(const bf16* src, size_t rows, int C, float* dst, hipStream_t s);

@@ -986,12 +986,30 @@ __device__ __forceinline__ void down0_positions(const Down0Args& a, const float*
   }
 }
 
-template <typename T, int KIND, int XS = 0>
-__global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvArgs<T> a) {
+// In-launch seam between two conv layers (PETDIFF_SEAM23, an experiment: DESIGN.md section 8).  Roles by
+// block index: blocks [0, n_prod) run the producer layer's tiles, the rest the consumer layer's.  A
+// producer tile, once every storing wave has drained its write-through (sc1) stores, adds 1 to the
+// counter of the consumer sample block it feeds; a consumer tile issues its first chunk's weight DMA,
+// then one lane per loader wave polls its sample block's counter (sc1 loads, s_sleep, a bounded spin that
+// records a give-up in err instead of hanging), takes an agent-scope acquire and only then issues its
+// activation DMA.  The last consumer to finish zeroes the counters for the next launch.
+struct SeamArgs {
+  int* grp = nullptr;        // [consumer sample blocks] producer tiles done
+  int* done = nullptr;       // consumer tiles done (the last one resets grp and done)
+  int* err = nullptr;        // spins given up (0 in a correct run)
+  int n_prod = 0;            // producer tiles (= consumer block index offset)
+  int n_cons = 0;            // consumer tiles
+  int n_grp = 0;             // consumer sample blocks
+  int per_grp = 0;           // producer tiles per full sample block
+  int n_prod_m = 0;          // producer M tiles (the last sample block may have fewer)
+  int prod_n = 0;            // producer N tiles
+};
+
+template <typename T, int KIND, int XS, int SEAM>
+__device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int bid, const SeamArgs sa) {
   using G = ConvGeom<T, KIND>;
   constexpr int L = G::L, TAPS = G::TAPS, PADL = G::PADL, EPI = G::EPI, ROWB = G::ROWB, NT = G::NT;
   constexpr bool UPS = G::UPS;
-  __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
 
   const int tid = threadIdx.x;
 #if CONV_EXP_MODE & 128
@@ -1014,7 +1032,6 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
   const int nM = (B + G::S - 1) / G::S;
   const int nN = a.cout / NT;
   const int total = nM * nN;
-  const int bid = blockIdx.x;
   const int xcd = bid & 7, loc = bid >> 3, q8 = total >> 3, r8 = total & 7;
 #ifndef CONV_XCD_MAP
 #define CONV_XCD_MAP 1    // 0: identity, 1: XCD-contiguous slots N-fastest, 2: XCD-contiguous slots M-fastest,
@@ -1745,7 +1762,28 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
       else if (NC > 1) ring_barrier<G::PER>();
       else ring_barrier<0>();
 #else
-      dma.all(smem, 0, 0, lane);
+      if constexpr (SEAM == 2) {
+        // seam consumer: chunk 0's weights first, then wait for the producers of this tile's samples
+#pragma unroll
+        for (int k = G::APT; k < G::PER; ++k) dma.piece(smem, k, 0, lane);
+        const int g = m_tile, want = sa.prod_n * min(sa.per_grp / sa.prod_n, sa.n_prod_m - g * (sa.per_grp / sa.prod_n));
+        if (lane == 0) {
+          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+          while (__hip_atomic_load(sa.grp + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {   // 20 ms: give up, do not hang
+              __hip_atomic_fetch_add(sa.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < G::APT; ++k) dma.piece(smem, k, 0, lane);
+      } else {
+        dma.all(smem, 0, 0, lane);
+      }
       ring_barrier<0>();                                   // B0: chunk 0 landed
       if (NC > 1) dma.all(smem, 1, 1, lane);
       if (NC > 2) dma.all(smem, 2, 2, lane);
@@ -2020,6 +2058,24 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
     if (mode == 1) epi_rows(std::integral_constant<int, 1>{});
     else if (mode == 2) epi_rows(std::integral_constant<int, 2>{});
     else epi_rows(std::integral_constant<int, 0>{});
+    if constexpr (SEAM != 0) {
+      // every storing wave drains its write-through stores; then one lane signals for the workgroup
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        if constexpr (SEAM == 1) {
+          __hip_atomic_fetch_add(sa.grp + m_tile / (sa.per_grp / sa.prod_n), 1, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          // the last consumer resets the counters for the next launch (every producer has signalled by
+          // then: every consumer waited for its producers)
+          if (__hip_atomic_fetch_add(sa.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == sa.n_cons - 1) {
+            for (int k = 0; k < sa.n_grp; ++k) __hip_atomic_store(sa.grp + k, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(sa.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+      }
+    }
 #if CONV_EXP_MODE & 128
     if (tid == 0) reinterpret_cast<unsigned long long*>(a.fin.x_all)[4096 + 2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
@@ -2209,6 +2265,24 @@ __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvA
 #endif
     }
   }
+}
+
+template <typename T, int KIND, int XS = 0>
+__global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvArgs<T> a) {
+  __shared__ __attribute__((aligned(16))) char smem[ConvGeom<T, KIND>::SMEM];
+  conv_body<T, KIND, XS, 0>(a, smem, blockIdx.x, SeamArgs{});
+}
+
+// down2 -> down3 in one launch (SeamArgs): blocks [0, n_prod) = down2 tiles, the rest down3 tiles
+template <typename T, int XS>
+__global__ __launch_bounds__(2 * kThreads, 1) void seam23_kernel(ConvArgs<T> a2, ConvArgs<T> a3, SeamArgs sa) {
+  constexpr int S2 = ConvGeom<T, LK_DOWN2>::SMEM, S3 = ConvGeom<T, LK_DOWN3>::SMEM;
+  static_assert(ConvGeom<T, LK_DOWN2>::NTH == 2 * kThreads && ConvGeom<T, LK_DOWN3>::NTH == 2 * kThreads,
+                "both layers run the 8-wave loader shape");
+  __shared__ __attribute__((aligned(16))) char smem[S2 > S3 ? S2 : S3];
+  const int b = blockIdx.x;
+  if (b < sa.n_prod) conv_body<T, LK_DOWN2, XS, 1>(a2, smem, b, sa);
+  else conv_body<T, LK_DOWN3, XS, 2>(a3, smem, b - sa.n_prod, sa);
 }
 
 // ---------------------------------------------------------------------------
@@ -2485,6 +2559,12 @@ static hipError_t launch_one(const ConvArgs<T>& a, hipStream_t s) {
 }
 
 template <typename T, int XS>
+static hipError_t launch_seam23_xs(const ConvArgs<T>& a2, const ConvArgs<T>& a3, const SeamArgs& sa, hipStream_t s) {
+  hipLaunchKernelGGL((seam23_kernel<T, XS>), dim3(sa.n_prod + sa.n_cons), dim3(2 * kThreads), 0, s, a2, a3, sa);
+  return hipGetLastError();
+}
+
+template <typename T, int XS>
 static hipError_t launch_conv_xs(int kind, const ConvArgs<T>& a, hipStream_t s) {
   switch (kind) {
     case LK_DOWN1: return launch_one<T, LK_DOWN1, XS>(a, s);
@@ -2532,6 +2612,38 @@ hipError_t launch_down0(const Down0Args& a, hipStream_t s, bool x3) {
   return hipGetLastError();
 }
 
+// down2 + down3 in one launch (PETDIFF_SEAM23); seam_state: int [n_grp + 2] zeroed once at allocation
+template <typename T>
+hipError_t launch_seam23(const ConvArgs<T>& a2, const ConvArgs<T>& a3, int* seam_state, hipStream_t s, bool x3) {
+  if constexpr (sizeof(T) != 2) {
+    return hipErrorInvalidValue;
+  } else {
+    using G2 = ConvGeom<T, LK_DOWN2>;
+    using G3 = ConvGeom<T, LK_DOWN3>;
+    if (a2.B <= 0) return hipSuccess;
+    static_assert(G3::S % G2::S == 0, "a down3 sample block is whole down2 M tiles");
+    SeamArgs sa;
+    const int n2m = (a2.B + G2::S - 1) / G2::S, n3m = (a3.B + G3::S - 1) / G3::S;
+    sa.prod_n = a2.cout / G2::NT;
+    sa.n_prod = n2m * sa.prod_n;
+    sa.n_cons = n3m * (a3.cout / G3::NT);
+    sa.n_grp = n3m;
+    sa.per_grp = (G3::S / G2::S) * sa.prod_n;
+    sa.n_prod_m = n2m;
+    sa.grp = seam_state;
+    sa.done = seam_state + n3m;
+    sa.err = seam_state + n3m + 1;
+    if (a2.cout % G2::NT || a3.cout % G3::NT || a2.c1 % G2::KC || a3.c1 % G3::KC) return hipErrorInvalidValue;
+    if (x3) {
+      if constexpr (std::is_same<T, bf16>::value) return launch_seam23_xs<T, 1>(a2, a3, sa, s);
+      return hipErrorInvalidValue;
+    }
+    return launch_seam23_xs<T, 0>(a2, a3, sa, s);
+  }
+}
+template hipError_t launch_seam23<bf16>(const ConvArgs<bf16>&, const ConvArgs<bf16>&, int*, hipStream_t, bool);
+template hipError_t launch_seam23<f16>(const ConvArgs<f16>&, const ConvArgs<f16>&, int*, hipStream_t, bool);
+template hipError_t launch_seam23<float>(const ConvArgs<float>&, const ConvArgs<float>&, int*, hipStream_t, bool);
 template hipError_t launch_conv<bf16>(int, const ConvArgs<bf16>&, hipStream_t, bool);
 template hipError_t launch_conv<f16>(int, const ConvArgs<f16>&, hipStream_t, bool);
 template hipError_t launch_conv<float>(int, const ConvArgs<float>&, hipStream_t, bool);

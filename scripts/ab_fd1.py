@@ -1,7 +1,8 @@
-"""In-process A/B of the fused next-step down1 (PETDIFF_FUSE_DOWN1=1) against the standalone down1 launch
-(=0), per dtype: configs[1] workload (1 TAC x 1024 samples x 1000 steps, graph), rounds interleaved, plus
-per-layer HIP-event times of one eager generate per variant.  The library under test is PETDIFF_LIB (or the
-in-tree build).  Usage: python scripts/ab_fd1.py OUT.jsonl [dtypes...]"""
+"""In-process A/B of a handle switch read at creation (default PETDIFF_FUSE_DOWN1: the fused next-step down1
+against the standalone down1 launch; AB_VAR=PETDIFF_SEAM23 etc.), per dtype: configs[1] workload (1 TAC x
+1024 samples x 1000 steps, graph), rounds interleaved, plus per-layer HIP-event times of one eager generate
+per variant and a bitwise check of a 20-step loop.  The library under test is PETDIFF_LIB (or the in-tree
+build).  Usage: [AB_VAR=...] python scripts/ab_fd1.py OUT.jsonl [dtypes...]"""
 import json
 import os
 import sys
@@ -10,6 +11,9 @@ import time
 import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
+
+
+VAR = os.environ.get('AB_VAR', 'PETDIFF_FUSE_DOWN1')
 
 
 def main(out, dtypes):
@@ -25,7 +29,7 @@ def main(out, dtypes):
     for dt in dtypes:
         models = {}
         for fuse in ('1', '0'):
-            os.environ['PETDIFF_FUSE_DOWN1'] = fuse
+            os.environ[VAR] = fuse
             m = ImprovedDDPM(network=net, dtype=dt, **shipped_diff_args())
             m._ensure_handle()
             x = m.philox_normal(B, seed=1)
@@ -49,14 +53,14 @@ def main(out, dtypes):
             lay[k] = {n: round(v[0] / max(v[1], 1) * 1e3, 2) for n, v in t.items() if v[1]}
         same = bool(torch.equal(models['1'][0].ddpm_loop(models['1'][1], cond[None], seed=3, num_timesteps=20),
                                 models['0'][0].ddpm_loop(models['0'][1], cond[None], seed=3, num_timesteps=20)))
-        rec = {'dtype': dt, 'lib': os.environ.get('PETDIFF_LIB', 'in-tree'), 'samples_per_s_fused': res['1'],
+        rec = {'switch': VAR, 'dtype': dt, 'lib': os.environ.get('PETDIFF_LIB', 'in-tree'), 'samples_per_s_fused': res['1'],
                'samples_per_s_standalone': res['0'], 'layer_us_fused': lay['1'], 'layer_us_standalone': lay['0'],
                'bitwise_equal_20_steps': same}
         print(json.dumps(rec), flush=True)
         f.write(json.dumps(rec) + '\n')
         for m, _ in models.values():
             m.close()
-    os.environ.pop('PETDIFF_FUSE_DOWN1', None)
+    os.environ.pop(VAR, None)
 
 
 if __name__ == '__main__':

@@ -4,6 +4,6 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r3train
-timeout -k 10 1120 python -u scripts/train_protocol.py gpurun_out/r3train --epochs 500 --eval-tacs 8 --period 100000 \
+timeout -k 10 1120 python -u scripts/train_protocol.py gpurun_out/r3train --epochs 500 --eval-tacs 8 --period 100000 --mh-textbook \
   --time-budget 880 > gpurun_out/r3train/train_log.txt 2>&1
 echo EXIT $?

@@ -13,7 +13,7 @@ run the reference's protocol (4 chains x (20,000 draws + 40,000 tune), mcmc.py:1
   0..L if the sampler is calibrated), coverage of the central 50 % / 90 % intervals, mean |z| with
   z = (truth - posterior mean) / posterior SD (0.80 for a calibrated Gaussian posterior).
 
-Usage: python scripts/mcmc_calibration.py OUT.json [--tacs 32] [--draws 20000] [--tune 40000]
+Usage: python scripts/mcmc_calibration.py OUT.json [--tacs 32] [--draws 20000] [--tune 40000] [--textbook]
 """
 import argparse
 import json
@@ -36,6 +36,8 @@ def main():
     ap.add_argument('--chains', type=int, default=4)
     ap.add_argument('--thin-to', type=int, default=999, help='L: thinned draws per TAC for the SBC rank')
     ap.add_argument('--seed0', type=int, default=7000)
+    ap.add_argument('--textbook', action='store_true',
+                    help="element ratios against the running state instead of PyMC's sweep-start point")
     args = ap.parse_args()
     from pet_posterior_distribution_amd.mcmc import MetropolisSRTM2
     from pet_posterior_distribution_amd.metrics import effective_sample_size
@@ -51,7 +53,7 @@ def main():
                  y_obs=cond[:48].astype(np.float64), sigma_noise=tr['sigma_noise'], mu_DVR=prior['mu_DVR'],
                  Cov_DVR=prior['Cov_DVR'], mu_R1=prior['mu_R1'], Cov_R1=prior['Cov_R1'])
         truth = np.concatenate([tr['DVR'], tr['R1']])
-        mh = MetropolisSRTM2(**P)
+        mh = MetropolisSRTM2(**P, vs_sweep_start=not args.textbook)
         t0 = time.perf_counter()
         res = mh.run(args.chains, args.draws, args.tune, seed=seed, return_draws=True)
         torch.cuda.synchronize()
@@ -94,6 +96,8 @@ def main():
     chi = float(((hist - exp) ** 2 / exp).sum())
     summary = {
         'protocol': f'{args.chains} chains x ({args.draws} draws + {args.tune} tune), mcmc.py:156-157',
+        'sampler': 'textbook element-wise Metropolis (ratio vs the running state)' if args.textbook else
+                   "PyMC 5.12 Metropolis elemwise_update (ratio vs the sweep-start point, delta_logp(q_temp, q0))",
         'prior': 'reference prior_stats_nROI48 (sim_data.reference_prior); truth = MvN restricted to DVR, R1 > 0',
         'tacs': args.tacs, 'seconds': round(time.perf_counter() - t_all, 1),
         'rhat_flagged_tacs': int(sum(r['rhat_flag_gt_1.02'] for r in per_tac)),

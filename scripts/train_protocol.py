@@ -64,6 +64,8 @@ def main():
     ap.add_argument('--mh-draws', type=int, default=20000)
     ap.add_argument('--mh-tune', type=int, default=40000)
     ap.add_argument('--f32-eval', action='store_true', help='also sample the posterior with the exact-f32 network')
+    ap.add_argument('--mh-textbook', action='store_true',
+                    help="also score against the MH with the textbook element ratio (PyMC's is against the sweep start)")
     ap.add_argument('--test-source', default='train-generator', choices=['train-generator', 'independent'],
                     help='train-generator: unseen TACs from the training generator (same per-ROI noise level as the '
                          'training set, the likelihood the network learned); independent: a TAC with its own noise '
@@ -152,6 +154,14 @@ def main():
         rec['mcmc_rhat_max'] = round(conv['rhat_max'], 5)
         rec['mcmc_rhat_flag_gt_1.02'] = conv['flag']
         draws = res['draws']
+        tb_draws = None
+        if args.mh_textbook:   # the same chains with the textbook element ratio (against the running state)
+            mh_tb = MetropolisSRTM2(**P, vs_sweep_start=False)
+            rtb = mh_tb.run(4, args.mh_draws, args.mh_tune, seed=3 + k, return_draws=True)
+            tb_draws = rtb['draws']
+            rec['mcmc_textbook_rhat_max'] = round(rtb['convergence']['rhat_max'], 5)
+            mh_tb.close()
+        mh.close()
         for tag, dt in samplers:
             m = ImprovedDDPM(network=net, dtype=dt, **shipped_diff_args())
             x_T = m.philox_normal(args.n_posterior, seed=1 + k)
@@ -187,6 +197,17 @@ def main():
                  'mcmc_mean_abs_err_vs_truth': {
                      'DVR': round(float(np.mean(np.abs(dr[..., :48].reshape(-1, 48).mean(0) - truth['DVR']))), 5),
                      'R1': round(float(np.mean(np.abs(dr[..., 48:].reshape(-1, 48).mean(0) - truth['R1']))), 5)}}
+            if tb_draws is not None:
+                mt = posterior_metrics(x0, tb_draws)
+                r['vs_textbook_mh'] = {
+                    'norm_diff': {name: {q: round(float(np.mean(mt[name][q]['Norm_diff'])), 5) for q in ('mu', 'std')}
+                                  for name in ('DVR', 'R1')},
+                    'std_ratio_nn_over_mcmc_mean': {
+                        name: round(float(np.mean(mt[name]['std']['NN'] / mt[name]['std']['MCMC'])), 4)
+                        for name in ('DVR', 'R1')},
+                    'mcmc_calibration': {name: round(float(np.mean(np.abs(truth[name][:, None] - mt[name]['mu']['MCMC'])
+                                                                  / mt[name]['std']['MCMC'])), 4)
+                                         for name in ('DVR', 'R1')}}
             rec[tag] = r
             m.close()
             print(json.dumps({'tac': seed, tag: r}), flush=True)

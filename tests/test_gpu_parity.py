@@ -388,6 +388,35 @@ def test_fused_next_step_down1_bitwise(conds, dtype, monkeypatch):
     fused.close()
 
 
+@pytest.mark.parametrize('dtype', ['bfloat16', 'float16', 'bf16x3'])
+def test_seam23_bitwise(conds, dtype, monkeypatch):
+    """PETDIFF_SEAM23=1 runs down2 and down3 in one launch (blocks [0, n) = down2 tiles; a down3 tile waits on
+    a per-sample-block counter of the down2 tiles that feed it, then acquires).  Same per-tile arithmetic as
+    the two launches: bit-identical forward (ragged batches: a last sample block with one down2 M tile) and
+    graph loops, repeated launches (the counters reset themselves)."""
+    rng = np.random.default_rng(27)
+    monkeypatch.setenv('PETDIFF_SEAM23', '0')
+    plain = make_model(dtype)
+    plain._ensure_handle()
+    monkeypatch.setenv('PETDIFF_SEAM23', '1')
+    seam = make_model(dtype)
+    seam._ensure_handle()
+    table = np.stack([conds[0], conds[1]])
+    for B in (5, 37, 96, 1024):
+        x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+        t = rng.integers(0, 1000, B).astype(np.int32)
+        cond = table[rng.integers(0, 2, B)]
+        torch.testing.assert_close(plain.call({'x': x, 'time': t, 'condition': cond}),
+                                   seam.call({'x': x, 'time': t, 'condition': cond}), rtol=0, atol=0)
+    x = rng.standard_normal((256, 48, 2)).astype(np.float32)
+    for _ in range(2):
+        a = plain.ddpm_loop(x, conds[:1], num_timesteps=30, seed=4)
+        b = seam.ddpm_loop(x, conds[:1], num_timesteps=30, seed=4)
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    plain.close()
+    seam.close()
+
+
 def test_split_streams_bitwise(conds, monkeypatch):
     """PETDIFF_SPLIT=2 runs the batch as two sample ranges, each its own graph on its own
     stream: identical samples to the single-graph run (counter-based noise, per-sample math)."""
