@@ -990,9 +990,9 @@ __device__ __forceinline__ void down0_positions(const Down0Args& a, const float*
 // block index: blocks [0, n_prod) run the producer layer's tiles, the rest the consumer layer's.  A
 // producer tile, once every storing wave has drained its write-through (sc1) stores, adds 1 to the
 // counter of the consumer sample block it feeds; a consumer tile issues its first chunk's weight DMA,
-// then one lane per loader wave polls its sample block's counter (sc1 loads, s_sleep, a bounded spin that
-// records a give-up in err instead of hanging), takes an agent-scope acquire and only then issues its
-// activation DMA.  The last consumer to finish zeroes the counters for the next launch.
+// then lane 0 of loader wave 0 polls its sample block's counter (sc1 loads, s_sleep, a bounded spin that
+// records a give-up in err instead of hanging), that wave takes the agent-scope acquire (one L1 invalidate
+// per CU), a workgroup barrier releases the other waves, and only then is the activation DMA issued.  The last consumer to finish zeroes the counters for the next launch.
 struct SeamArgs {
   int* grp = nullptr;        // [consumer sample blocks] producer tiles done
   int* done = nullptr;       // consumer tiles done (the last one resets grp and done)
@@ -1767,18 +1767,29 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
 #pragma unroll
         for (int k = G::APT; k < G::PER; ++k) dma.piece(smem, k, 0, lane);
         const int g = m_tile, want = sa.prod_n * min(sa.per_grp / sa.prod_n, sa.n_prod_m - g * (sa.per_grp / sa.prod_n));
-        if (lane == 0) {
-          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-          while (__hip_atomic_load(sa.grp + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-            __builtin_amdgcn_s_sleep(2);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {   // 20 ms: give up, do not hang
-              __hip_atomic_fetch_add(sa.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              break;
+#ifndef CONV_SEAM_ONE_FENCE
+#define CONV_SEAM_ONE_FENCE 1   // 1: loader wave 0 polls and acquires for the CU, a workgroup barrier releases the
+                                //    other waves (the MFMA waves join it before B0); 0: every loader wave polls and
+                                //    acquires (4 L1 invalidates per CU: about 9 us of prologue, scripts/micro/seam_micro)
+#endif
+        if (!CONV_SEAM_ONE_FENCE || w == 0) {
+          if (lane == 0) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(sa.grp + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+              __builtin_amdgcn_s_sleep(2);
+              if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {   // 20 ms: give up, do not hang
+                __hip_atomic_fetch_add(sa.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+              }
             }
+#if CONV_EXP_MODE & 128
+            if (w == 0) reinterpret_cast<unsigned long long*>(a.fin.x_all)[12288 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
           }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // this CU's L1 (one invalidate covers every wave)
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // ... and it has completed
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (CONV_SEAM_ONE_FENCE) __builtin_amdgcn_s_barrier();  // the seam barrier (MFMA waves: before B0)
 #pragma unroll
         for (int k = 0; k < G::APT; ++k) dma.piece(smem, k, 0, lane);
       } else {
@@ -1795,6 +1806,9 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       }
     } else {
       prefetch_maps();
+      if constexpr (SEAM == 2) {
+        if (CONV_SEAM_ONE_FENCE) __builtin_amdgcn_s_barrier();   // the seam barrier: loader wave 0 has acquired
+      }
       ring_barrier<0>();                                   // B0 (maps landed too)
 #if CONV_EXP_MODE & 128
       st_c0 = __builtin_amdgcn_s_memtime();
