@@ -2,8 +2,8 @@
 
 Reference protocol (yanisdjebra/PET_posterior_distribution):
 * data: sample_sim_data.py:89-215 -- 100,000 simulated TACs (truncated-MvN prior, SRTM2, truncated noise);
-  here the GPU generator (sim_data.simulate_dataset) on the synthetic prior
-  (the reference's prior pickle is not loaded: no unpickling of reference files);
+  here the GPU generator (sim_data.simulate_dataset) on the reference prior
+  (sim_data.reference_prior: the prior_stats_nROI48 arrays, read by a static pickle parser, DESIGN.md section 4);
 * training: main_script.py:131-271 -- UnetConditional f128/d4, iDDPM T=1000 cosine, lambda_vlb 0.1,
   Adam(ExponentialDecay(2e-4 -> 5e-5 over 500 epochs), clipnorm 1.5), batch 256, 500 epochs,
   validation_split 0.1, WeightsCheckpoint every 50 epochs;
