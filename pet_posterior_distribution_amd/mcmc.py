@@ -22,6 +22,27 @@ from . import _lib
 from .distributed import merge_stats
 
 
+class CreateTAC_SRTM2:
+    """The MH model's SRTM2 forward op (mcmc.py:27-39), without PyTensor (absent here): (DVR (n_roi,),
+    R1 (n_roi,), k2p scalar) -> the (n_roi, 54) fp64 TAC, computed by ``k_srtm`` (kinetic_model.SRTM2, the
+    GPU SRTM2 kernel).  ``perform`` keeps the Op's calling convention (outputs[0][0] = the TAC); the
+    samplers below evaluate the same model inside their kernels and do not call it."""
+    __props__ = ()
+    itypes = ('dvector', 'dvector', 'dscalar')
+    otypes = ('dmatrix',)
+
+    def __init__(self, k_srtm):
+        self.k_srtm = k_srtm
+
+    def perform(self, node, inputs, outputs, **kwargs):
+        outputs[0][0] = self.k_srtm.create_activity_curve(DVR=inputs[0], R1=inputs[1], k2p=inputs[2]).T
+
+    def __call__(self, DVR, R1, k2p):
+        out = [[None]]
+        self.perform(None, (DVR, R1, k2p), out)
+        return out[0][0]
+
+
 class MetropolisSRTM2:
     def __init__(self, time_vector, tac_ref, k2p, y_obs, sigma_noise, mu_DVR, Cov_DVR, mu_R1, Cov_R1, device=None,
                  tune_interval=100, scaling=1.0, vs_sweep_start=True, kernel='auto', waves_per_chain=0):

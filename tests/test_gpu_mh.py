@@ -36,6 +36,22 @@ def test_srtm2_kernel_vs_reference(g2):
         np.testing.assert_allclose(tac, g2[f'case{k}_tac'], rtol=1e-10, atol=1e-12)
 
 
+def test_create_tac_op_vs_reference(g2):
+    """mcmc.CreateTAC_SRTM2 (the reference's PyTensor Op, mcmc.py:27-39) through its perform() calling
+    convention and as a callable: the (n_roi, 54) TAC of the reference's kinetic_model outputs (G2)."""
+    from pet_posterior_distribution_amd.kinetic_model import SRTM2
+    from pet_posterior_distribution_amd.mcmc import CreateTAC_SRTM2
+    tv, dt = g2['time_vector'], g2['dt']
+    for k in range(4):
+        op = CreateTAC_SRTM2(SRTM2(tv, dt, g2[f'case{k}_tac_ref']))
+        args = (g2[f'case{k}_DVR'], g2[f'case{k}_R1'], float(g2[f'case{k}_k2p']))
+        out = [[None]]
+        op.perform(None, args, out)
+        assert out[0][0].shape == (48, 54)
+        np.testing.assert_allclose(out[0][0], g2[f'case{k}_tac'].T, rtol=1e-10, atol=1e-12)
+        np.testing.assert_array_equal(op(*args), out[0][0])
+
+
 def test_srtm2_batched(g2):
     from pet_posterior_distribution_amd.kinetic_model import SRTM2
     tv, dt = g2['time_vector'], g2['dt']
