@@ -106,6 +106,19 @@
 #ifndef CONV_DOWN1_PP
 #define CONV_DOWN1_PP 0
 #endif
+// up0 fused level, zero (fragment, tap) products skipped.  A fragment is one coarse row m of 32
+// samples (fine position l = 2m + e), so a (fragment, tap) MFMA either reads data or the zero row:
+// segment 1 (skip s2, 6 taps at l) reads padding at l = 0, 1, 9, 10, 11 (9 of 72 products),
+// segment 2 (coarse b, 4 composite taps at m) at m = 0 (tap 0, which the left-edge correction
+// covers), m = 4, 5 (3 of 24).  The waves keep their output phase e (segment 2's B taps are per
+// phase) and take the coarse rows {0, 4, 1} / {5, 2, 3}, which balances the zeros: per k-group the
+// slowest wave runs 16 of 18 segment-1 and 11 of 13 segment-2 (incl. correction) products instead
+// of 18 and 13.  Each wave runs a main loop specialised on its set (no per-step branch); the MFMA
+// order per accumulator is the tap-reuse path's, so the results are bitwise unchanged.
+// 0 = the tap-reuse path (every product, consecutive rows {0, 1, 2} / {3, 4, 5}).
+#ifndef CONV_UP0_ZS
+#define CONV_UP0_ZS 1
+#endif
 
 namespace petdiff {
 
@@ -354,6 +367,23 @@ struct ConvGeom {
   static constexpr bool AFULL2 = true;
   static constexpr int PER2 = APT2 + BPT2;          // segment-2 chunks
   static constexpr int PHROWS = FUSED ? S * LH : MT; // tile rows per output phase (fused)
+  // up0 zero-skip (CONV_UP0_ZS): wave wm computes phase wm >> 1, coarse rows zs_m(wm & 1, i)
+  static constexpr bool ZS = CONV_UP0_ZS && FUSED && S == 32 && L == 12 && sizeof(T) == 2 && STAGES == 3;
+  static constexpr __device__ __host__ int zs_m(int set, int i) {
+    return set == 0 ? (i == 0 ? 0 : i == 1 ? 4 : 1) : (i == 0 ? 5 : i == 1 ? 2 : 3);
+  }
+  // (fragment i, segment-1 tap j) / (fragment i, composite tap k) of wave pat reads data
+  static constexpr __device__ __host__ bool zs_valid1(int pat, int i, int j) {
+    return 2 * zs_m(pat & 1, i) + (pat >> 1) + j - PADL >= 0 && 2 * zs_m(pat & 1, i) + (pat >> 1) + j - PADL < L;
+  }
+  static constexpr __device__ __host__ bool zs_valid2(int pat, int i, int k) {
+    return zs_m(pat & 1, i) - 1 + k >= 0 && zs_m(pat & 1, i) - 1 + k < LH;
+  }
+  // first tile row of wave wm's fragment i (tile rows stay [phase][m][sample] for the epilogue)
+  static __device__ __forceinline__ int frag_row(int wm, int i) {
+    if constexpr (ZS) return (wm >> 1) * PHROWS + zs_m(wm & 1, i) * S;
+    else return wm * 96 + i * 32;
+  }
   static constexpr int CT_LD = 2 * NT + 8;          // fp32 C tile, one ROW PAIR [c][2] per line (non-final)
   static constexpr int FIN_LD = 132;                // fp32 C tile row (final epilogue, 16-B aligned)
   // FINAL: C tile | final kernel [128][4] | x_next rows [MT][2] (fused next-step down0)
@@ -1106,12 +1136,13 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   const int c0 = (sizeof(T) == 2) ? h : 2 * h;
   const int wv = __builtin_amdgcn_readfirstlane(w);
   const int pm_pat = wv / G::SH;                    // position-major: this wave's fragment set
+  const int wmu = G::ZS ? wv / G::WN : wm;          // up0 zero-skip: the fragment set from the uniform index
   int aoff[TAPS][3];
 #pragma unroll
   for (int j = 0; j < TAPS; ++j) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      const int r = wm * 96 + i * 32 + lr;
+      const int r = G::frag_row(wmu, i) + lr;
       int s, l;
       if constexpr (G::PM) {   // wave-uniform position: scalar work, no divergent select chain
         l = G::pm_pos(pm_pat, i);
@@ -1148,14 +1179,14 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     for (int k = 0; k < G::TAPS2; ++k) {
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
-        const int r = wm * 96 + i * 32 + lr;
+        const int r = G::frag_row(wmu, i) + lr;
         const int sq = r % G::S, m = (r / G::S) % G::LH, q = m - 1 + k;
         const int row = q * G::S + sq;
         aoff2[k][i] = (q >= 0 && q < G::LH) ? row * ROWB + ((c0 ^ G::key(row)) << 4) : G::ZOFF + (c0 << 4);
       }
     }
     {
-      const int r = wm * 96 + lr;
+      const int r = G::frag_row(wmu, 0) + lr;
       const int sq = r % G::S, m = (r / G::S) % G::LH, row = sq;
       amask = m == 0 ? row * ROWB + ((c0 ^ G::key(row)) << 4) : G::ZOFF + (c0 << 4);
     }
@@ -1203,7 +1234,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   // (segment 1) or coarse row Q = i + k (segment 2) relative to its first fragment; each step
   // reads only the positions no earlier step of its k-group has read.  cav carries the last
   // step's A operands into the next chunk's first step (whose MFMAs they are).
-  constexpr bool REUSE = CONV_TAP_REUSE && G::FUSED && G::S == 32 && sizeof(T) == 2;
+  constexpr bool REUSE = CONV_TAP_REUSE && G::FUSED && G::S == 32 && sizeof(T) == 2 && !G::ZS;
   fragT cav[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) cav[i] = fragT{};
@@ -1239,9 +1270,110 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   // SEG = 2: a fused segment-2 chunk (4 composite taps of this wave's phase; kc = its index).
   auto compute = [&](const char* base, auto next_tag, int nkc, int nbuf, auto seg_tag, int kc, auto pat_tag) {
     constexpr int NEXT = (int)decltype(next_tag)::value;
-    constexpr int SEG = (int)decltype(seg_tag)::value;
+    // SEG: 1 / 2; seg_tag 4 = the first segment-2 chunk (up0 zero-skip: its step 0 carries segment 1's last step)
+    constexpr int SEGV = (int)decltype(seg_tag)::value;
+    constexpr int SEG = SEGV == 4 ? 2 : SEGV;
     char* nbase = smem + nbuf * G::STAGE;
-    if constexpr (REUSE) {
+    if constexpr (G::ZS) {
+      // up0 zero-skip: step st = (k-group g, tap tap_of(jj)) in the tap-reuse path's order; the MFMAs
+      // of step st - 1 and the reads of step st, both over the (fragment, tap) pairs that read data.
+      // At st = 0 the MFMAs are the previous chunk's last step, of segment 1 when this is the first
+      // segment-2 chunk (SEGV == 4: peeled at compile time; a runtime choice there made the compiler
+      // shuffle the accumulators between two register assignments every chunk).
+      constexpr int PAT = decltype(pat_tag)::value;
+      constexpr int NG = ROWB / 32;
+      constexpr int NT_ = SEG == 2 ? G::TAPS2 : TAPS;
+      constexpr int NS = NT_ * NG;
+      constexpr int NPER = NEXT == 3 ? G::PER2 : G::PER;
+      constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;
+      constexpr int PPS = (NPC + NS - 1) / NS;
+      constexpr bool M0 = (PAT & 1) == 0;                 // fragment 0 is coarse row 0 (edge correction)
+      static_assert(NS % 2 == 0, "fragment double buffer alternates per step");
+      fragT am[SEG == 2 ? NG : 1];
+      auto tap_of = [](int jj) { return SEG == 2 ? jj : (jj < 3 ? 2 * jj : 2 * (jj - 3) + 1); };
+      auto ok = [](int i, int j) { return SEG == 2 ? G::zs_valid2(PAT, i, j) : G::zs_valid1(PAT, i, j); };
+#pragma unroll
+      for (int st = 0; st < NS; ++st) {
+        const int g = st / NT_, jj = st % NT_, sb = st & 1, pb = sb ^ 1;
+        const int j = tap_of(jj);
+        const int jp = tap_of((st == 0 ? NS - 1 : st - 1) % NT_);
+        int ao0, ao1, ao2, bo0, bo1;
+        if constexpr (SEG == 2) {
+          ao0 = aoff2[j][0]; ao1 = aoff2[j][1]; ao2 = aoff2[j][2]; bo0 = boff2[0]; bo1 = boff2[1];
+        } else {
+          ao0 = aoff[j][0]; ao1 = aoff[j][1]; ao2 = aoff[j][2]; bo0 = boff[0]; bo1 = boff[1];
+        }
+        const char* pa0 = base + (ao0 ^ (g << 5));
+        const char* pa1 = base + (ao1 ^ (g << 5));
+        const char* pa2 = base + (ao2 ^ (g << 5));
+        const char* pb0 = base + ((bo0 + j * NT * ROWB) ^ (g << 5));
+        const char* pb1 = base + ((bo1 + j * NT * ROWB) ^ (g << 5));
+        // the MFMAs of step st - 1 (fragment i, B half jn) and the reads of step st
+        auto body = [&](auto prev_tag) {
+          constexpr int PV = decltype(prev_tag)::value;   // 0: this segment's step st - 1; 1: segment 1's last; 2: segment 2's last
+          auto okp = [&](int i) {
+            return PV == 1 ? G::zs_valid1(PAT, i, TAPS - 1) : PV == 2 ? G::zs_valid2(PAT, i, G::TAPS2 - 1) : ok(i, jp);
+          };
+#define PETDIFF_ZMF(i, jn)                                                                                 \
+  if (okp(i)) {                                                                                            \
+    if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(av[pb][i], bv[pb][jn], acc[i][jn]);            \
+  }
+#define PETDIFF_ZRD(dst, ptr, valid) \
+  if (valid) { if constexpr (!(CONV_EXP_MODE & 64)) dst = *reinterpret_cast<const fragT*>(ptr); }
+          PETDIFF_ZMF(0, 0)
+          PETDIFF_ZRD(av[sb][0], pa0, ok(0, j))
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_ZMF(0, 1)
+          PETDIFF_ZRD(bv[sb][0], pb0, true)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_ZMF(1, 0)
+          PETDIFF_ZRD(bv[sb][1], pb1, true)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_ZMF(1, 1)
+          PETDIFF_ZRD(av[sb][1], pa1, ok(1, j))
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_ZMF(2, 0)
+          PETDIFF_ZRD(av[sb][2], pa2, ok(2, j))
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_ZMF(2, 1)
+#undef PETDIFF_ZRD
+#undef PETDIFF_ZMF
+        };
+        if (st > 0) body(std::integral_constant<int, 0>{});
+        else if constexpr (SEG == 1 || SEGV == 4) body(std::integral_constant<int, 1>{});
+        else body(std::integral_constant<int, 2>{});
+        if constexpr (SEG == 2 && M0) {
+          // left-edge correction of the m = 0 rows, in the tap-reuse path's place: coarse row 0 read
+          // at step 0, multiplied after step 0's MFMAs (issued at step 1); then the next chunk's weights
+          if (st == 0) {
+#pragma unroll
+            for (int gg = 0; gg < NG; ++gg) am[gg] = *reinterpret_cast<const fragT*>(base + (amask ^ (gg << 5)));
+          }
+          if (st == 1) {
+#pragma unroll
+            for (int gg = 0; gg < NG; ++gg)
+#pragma unroll
+              for (int jn = 0; jn < 2; ++jn)
+                if constexpr (!(CONV_EXP_MODE & 2)) acc[0][jn] = mfma32(am[gg], epk[gg][jn], acc[0][jn]);
+            const int k2 = kc - dma.n1;
+            if (kc + 1 < NC) load_epk(k2 + 1);
+          }
+        }
+        if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
+#pragma unroll
+          for (int u = 0; u < PPS; ++u) {
+            const int k = st * PPS + u;
+            if (k < NPER) {
+              if constexpr (NEXT == 3) dma.piece2(nbase, k, nkc - dma.n1, lane);
+              else dma.piece1(nbase, k, nkc, lane);
+            } else if (NEXT == 2 && k < NPC) {
+              dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else if constexpr (REUSE) {
       constexpr int NG = ROWB / 32;
       constexpr int NT_ = SEG == 2 ? G::TAPS2 : TAPS;
       constexpr int NS = NT_ * NG;
@@ -1620,6 +1752,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
 #endif
   using Seg1 = std::integral_constant<int, 1>;
   using Seg2 = std::integral_constant<int, 2>;
+  using Seg2First = std::integral_constant<int, 4>;
   // fused final level, t uniform and one condition in the tile: map rows into LDS (FMAP_OFF)
   bool fin_fast = false;
   int tac0f = 0;
@@ -1708,29 +1841,55 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       st_c0 = __builtin_amdgcn_s_memtime();
       st_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
-      compute(smem, Two{}, 1, 1, Seg1{}, 0, P0{});              // chunks 1, 2 -> stages 1, 2
-      ring_barrier<G::PER>();
-      int buf = 1, kc = 1;
-      for (; kc + 2 < n1; ++kc) {
-        compute(smem + buf * G::STAGE, Yes{}, kc + 2, buf == 0 ? 2 : buf - 1, Seg1{}, 0, P0{});
+      auto fused_loop = [&](auto pat_tag) {
+        compute(smem, Two{}, 1, 1, Seg1{}, 0, pat_tag);              // chunks 1, 2 -> stages 1, 2
         ring_barrier<G::PER>();
+        int buf = 1, kc = 1;
+        for (; kc + 2 < n1; ++kc) {
+          compute(smem + buf * G::STAGE, Yes{}, kc + 2, buf == 0 ? 2 : buf - 1, Seg1{}, 0, pat_tag);
+          ring_barrier<G::PER>();
+          buf = buf == 2 ? 0 : buf + 1;
+        }
+        for (; kc < n1; ++kc) {                              // the next chunks are segment 2
+          compute(smem + buf * G::STAGE, Seg2Next{}, kc + 2, buf == 0 ? 2 : buf - 1, Seg1{}, 0, pat_tag);
+          ring_barrier<G::PER2>();
+          buf = buf == 2 ? 0 : buf + 1;
+        }
+        if constexpr (G::ZS) {   // the first segment-2 chunk, peeled (n2 >= 3: up0 has 32, bf16x3 96)
+          compute(smem + buf * G::STAGE, Seg2Next{}, kc + 2, buf == 0 ? 2 : buf - 1, Seg2First{}, kc, pat_tag);
+          ring_barrier<G::PER2>();
+          buf = buf == 2 ? 0 : buf + 1;
+          ++kc;
+        }
+        for (; kc + 2 < NC; ++kc) {
+          compute(smem + buf * G::STAGE, Seg2Next{}, kc + 2, buf == 0 ? 2 : buf - 1, Seg2{}, kc, pat_tag);
+          ring_barrier<G::PER2>();
+          buf = buf == 2 ? 0 : buf + 1;
+        }
+        compute(smem + buf * G::STAGE, No{}, 0, 0, Seg2{}, kc, pat_tag);
+        ring_barrier<0>();
         buf = buf == 2 ? 0 : buf + 1;
+        compute(smem + buf * G::STAGE, No{}, 0, 0, Seg2{}, kc + 1, pat_tag);
+        ring_barrier<0>();
+        if constexpr (G::ZS) {   // the last chunk's last step (composite tap 3) over this set's valid fragments
+          constexpr int PAT = decltype(pat_tag)::value;
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+            if (G::zs_valid2(PAT, i, G::TAPS2 - 1))
+#pragma unroll
+              for (int jn = 0; jn < 2; ++jn)
+                if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(av[1][i], bv[1][jn], acc[i][jn]);
+        }
+      };
+      // up0 zero-skip: each wave's fragment set gets its own main loop (no per-step branch)
+      if constexpr (G::ZS) {
+        if (wmu == 0) fused_loop(P0{});
+        else if (wmu == 1) fused_loop(std::integral_constant<int, 1>{});
+        else if (wmu == 2) fused_loop(std::integral_constant<int, 2>{});
+        else fused_loop(std::integral_constant<int, 3>{});
+      } else {
+        fused_loop(P0{});
       }
-      for (; kc < n1; ++kc) {                              // the next chunks are segment 2
-        compute(smem + buf * G::STAGE, Seg2Next{}, kc + 2, buf == 0 ? 2 : buf - 1, Seg1{}, 0, P0{});
-        ring_barrier<G::PER2>();
-        buf = buf == 2 ? 0 : buf + 1;
-      }
-      for (; kc + 2 < NC; ++kc) {
-        compute(smem + buf * G::STAGE, Seg2Next{}, kc + 2, buf == 0 ? 2 : buf - 1, Seg2{}, kc, P0{});
-        ring_barrier<G::PER2>();
-        buf = buf == 2 ? 0 : buf + 1;
-      }
-      compute(smem + buf * G::STAGE, No{}, 0, 0, Seg2{}, kc, P0{});
-      ring_barrier<0>();
-      buf = buf == 2 ? 0 : buf + 1;
-      compute(smem + buf * G::STAGE, No{}, 0, 0, Seg2{}, kc + 1, P0{});
-      ring_barrier<0>();
     }
   } else if constexpr (G::STAGES == 2) {
     dma.all(smem, 0, 0, lane);
@@ -1906,8 +2065,8 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
 #pragma unroll
       for (int jn = 0; jn < 2; ++jn)
         if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(cav[i], bv[1][jn], acc[i][jn]);
-  } else if constexpr (G::PM) {
-    // flushed at the end of the position-major main loop
+  } else if constexpr (G::PM || G::ZS) {
+    // flushed at the end of the position-major / zero-skip main loop
   } else {
     mfma_bf16(1);   // the last chunk's last step (NS even)
   }
@@ -1965,7 +2124,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       for (int jn = 0; jn < 2; ++jn)
 #pragma unroll
         for (int rg = 0; rg < 16; rg += 2) {
-          const int r = wm * 96 + i * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * h;   // even
+          const int r = G::frag_row(wmu, i) + (rg & 3) + 8 * (rg >> 2) + 4 * h;   // even
           *reinterpret_cast<float2*>(ct + (r >> 1) * G::CT_LD + (wn * 64 + jn * 32 + lr) * 2) =
               make_float2(acc[i][jn][rg], acc[i][jn][rg + 1]);
         }

@@ -4,7 +4,7 @@ change a single bit, e.g. CONV_DOWN2_PM: the zero taps a position-major tile ski
   python scripts/lib_bitwise.py dump out.npz        # with PETDIFF_LIB pointing at one build
   python scripts/lib_bitwise.py compare a.npz b.npz
 
-Covers: bf16 and fp16 forward on ragged batches (1, 37, 100, 1024) with interleaved per-sample
+Covers: bf16, fp16 and bf16x3 forward on ragged batches (1, 37, 100, 1024) with interleaved per-sample
 conditions and t (the general epilogue), one-condition forward (the LDS-map epilogue) and a
 20-step graph loop.
 """
@@ -19,7 +19,7 @@ def dump(path):
     from tests.helpers import synthetic_condition
     conds = np.stack([synthetic_condition(0), synthetic_condition(1)])
     res = {}
-    for dtype in ('bfloat16', 'float16'):
+    for dtype in ('bfloat16', 'float16', 'bf16x3'):
         m = make_model(dtype, seed=21)
         rng = np.random.default_rng(3)
         for B in (1, 37, 100, 1024):

@@ -206,6 +206,10 @@ int main(int argc, char** argv) {
     run<LK_UP2_F>("up2.fused", B, 128, 256, 128, it);
     return 0;
   }
+  if (std::string(only) == "u0") {   // the dominant level alone
+    run<LK_UP0_F>("up0.fused", B, 512, 1024, 512, it);
+    return 0;
+  }
   if (only[0] == 'f') {   // the product's 16-bit step: down layers + fused up levels
     run<LK_DOWN1>("down1", B, 128, 0, 256, it);
     run<LK_DOWN2>("down2", B, 256, 0, 512, it);
