@@ -187,14 +187,33 @@ int piece_key(int n, int cpr) { return cpr == 4 ? ((n >> 2) & 3) : cpr == 2 ? ((
 // K chunks of a packed weight tile in kernel order: (channel chunk, part) with part 0 = the value
 // (bf16x3: its hi half) and 1 = its lo half.  bf16x3 walks every input segment of nc chunks three
 // times -- (a_hi, w_hi), (a_hi, w_lo), (a_lo, w_hi) -- see DmaPlan in unet_kernels.hip.
-std::vector<std::pair<int, int>> chunk_order(int nc1, int nc2, bool x3) {
+// Paired bf16x3 (x3_paired(kind), petdiff_internal.h): part 2, the chunk index counts half chunks
+// (KC / 2 channels) whose rows hold [hi | lo].
+std::vector<std::pair<int, int>> chunk_order(int nc1, int nc2, bool x3, bool paired = false) {
   std::vector<std::pair<int, int>> o;
   for (int seg = 0; seg < 2; ++seg) {
     const int base = seg ? nc1 : 0, n = seg ? nc2 : nc1;
+    if (x3 && paired) {
+      for (int k = 0; k < 2 * n; ++k) o.push_back({2 * base + k, 2});
+      continue;
+    }
     for (int g = 0; g < (x3 ? 3 : 1); ++g)
       for (int k = 0; k < n; ++k) o.push_back({base + k, g == 1 ? 1 : 0});
   }
   return o;
+}
+
+// input channel and part (0 = the value / its hi half, 1 = its lo half) of element e of 16-B piece c
+// (CPR pieces of EPC elements per row) of chunk ck
+void chunk_elem(const std::pair<int, int>& ck, int KC, int CPR, int EPC, int c, int e, int& ch, int& part) {
+  if (ck.second == 2) {
+    const int hc = CPR / 2;
+    ch = ck.first * (KC / 2) + (c % hc) * EPC + e;
+    part = c >= hc;
+  } else {
+    ch = ck.first * KC + c * EPC + e;
+    part = ck.second;
+  }
 }
 
 float bf_hi(float v) { const uint32_t u = (uint32_t)f2bf(v) << 16; float f; std::memcpy(&f, &u, 4); return f; }
@@ -223,7 +242,7 @@ int pack_conv(petdiff_ctx* h, const std::vector<float>& wk_host, int li) {
   const int NC = cl.cin_x / KC, nNT = cl.cout / NT;
   // the up blocks read [skip | u] from two inputs of cin_x / 2 channels each (run_network's lio)
   const bool two = cl.xoff == 0 && cl.cond_level < 0;
-  const auto order = chunk_order(two ? NC / 2 : NC, two ? NC / 2 : 0, h->x3);
+  const auto order = chunk_order(two ? NC / 2 : NC, two ? NC / 2 : 0, h->x3, x3_paired(cl.kind));
   // [n_tile][chunk][tap][n (NT)][CPR x 16-B pieces], piece index XOR-swizzled by n
   // exactly like ConvGeom::key so a linear LDS-DMA copy yields the swizzled image.
   std::vector<H> out((size_t)nNT * order.size() * cl.taps * NT * KC);
@@ -235,11 +254,13 @@ int pack_conv(petdiff_ctx* h, const std::vector<float>& wk_host, int li) {
           for (int p = 0; p < CPR; ++p) {
             const int c = p ^ piece_key(n, CPR);
             for (int e = 0; e < EPC; ++e) {
-              const int ci = cl.xoff + ck.first * KC + c * EPC + e;
+              int ch, part;
+              chunk_elem(ck, KC, CPR, EPC, c, e, ch, part);
+              const int ci = cl.xoff + ch;
               const int co = nt * NT + n;
               float v = wk[((size_t)j * cl.cin_full + ci) * cl.cout + co];
               if (wr && j == cl.padl) v += wr[(size_t)ci * cl.cout + co];
-              v = split_part(v, ck.second);
+              v = split_part(v, part);
               if constexpr (std::is_same<T, f16>::value) out[q++] = f2h(v);
               else if constexpr (sizeof(H) == 2) out[q++] = f2bf(v);
               else out[q++] = v;
@@ -289,10 +310,10 @@ int pack_fused(petdiff_ctx* h, const std::vector<float>& host, int u) {
     if constexpr (std::is_same<T, f16>::value) return f2h(v);
     else return f2bf(v);
   };
-  const int x3 = h->x3 ? 3 : 1;
-  const auto order1 = chunk_order(n1, 0, h->x3), order2 = chunk_order(n2, 0, h->x3);
-  std::vector<H> out((size_t)nNT * x3 * (n1 * 6 + n2 * 8) * NT * KC);
-  std::vector<H> eout((size_t)nNT * x3 * n2 * 2 * NT * KC);
+  const bool pr = x3_paired(fl.kind);
+  const auto order1 = chunk_order(n1, 0, h->x3, pr), order2 = chunk_order(n2, 0, h->x3, pr);
+  std::vector<H> out((size_t)nNT * (order1.size() * 6 + order2.size() * 8) * NT * KC);
+  std::vector<H> eout((size_t)nNT * order2.size() * 2 * NT * KC);
   size_t q = 0, qe = 0;
   for (int nt = 0; nt < nNT; ++nt) {
     for (const auto& ck : order1)
@@ -301,28 +322,33 @@ int pack_fused(petdiff_ctx* h, const std::vector<float>& host, int u) {
           for (int p = 0; p < CPR; ++p) {
             const int c = p ^ piece_key(n, CPR);
             for (int e = 0; e < EPC; ++e) {
-              const int ci = ck.first * KC + c * EPC + e, co = nt * NT + n;
+              int ci, part;
+              chunk_elem(ck, KC, CPR, EPC, c, e, ci, part);
+              const int co = nt * NT + n;
               float v = wk[((size_t)j * blk.cin_full + ci) * blk.cout + co];
               if (j == blk.padl) v += wr[(size_t)ci * blk.cout + co];
-              out[q++] = cvt(split_part(v, ck.second));
+              out[q++] = cvt(split_part(v, part));
             }
           }
     for (const auto& ck : order2) {
-      const int kc = ck.first;
       for (int t = 0; t < 8; ++t)
         for (int n = 0; n < NT; ++n)
           for (int p = 0; p < CPR; ++p) {
             const int c = p ^ piece_key(n, CPR);
             for (int e = 0; e < EPC; ++e) {
-              const int cb = kc * KC + c * EPC + e, co = nt * NT + n;
-              out[q++] = cvt(split_part(D[((size_t)t * fl.cb + cb) * fl.cout + co], ck.second));
+              int cb, part;
+              chunk_elem(ck, KC, CPR, EPC, c, e, cb, part);
+              const int co = nt * NT + n;
+              out[q++] = cvt(split_part(D[((size_t)t * fl.cb + cb) * fl.cout + co], part));
             }
           }
       for (int ph = 0; ph < 2; ++ph)
         for (int n = 0; n < NT; ++n)
-          for (int kk = 0; kk < KC; ++kk)
-            eout[qe++] = cvt(split_part(D[((size_t)(8 + ph) * fl.cb + kc * KC + kk) * fl.cout + nt * NT + n],
-                                        ck.second));
+          for (int kk = 0; kk < KC; ++kk) {
+            int cb, part;
+            chunk_elem(ck, KC, CPR, EPC, kk / EPC, kk % EPC, cb, part);
+            eout[qe++] = cvt(split_part(D[((size_t)(8 + ph) * fl.cb + cb) * fl.cout + nt * NT + n], part));
+          }
     }
   }
   HIPC(h->wpack_f[u].alloc(out.size() * sizeof(H)));

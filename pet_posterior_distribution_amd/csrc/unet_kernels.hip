@@ -512,10 +512,15 @@ __device__ __forceinline__ void ring_barrier() {
 // [hi(C) | lo(C)] bf16 (hi = bf16(v), lo = bf16(v - hi)), and every input segment of C channels
 // is walked as 3 x C/KC chunks: (a_hi, w_hi), (a_hi, w_lo), (a_lo, w_hi) -- the same bf16 MFMA
 // loop over three times the chunks, fp32 accumulation (lo x lo, about 2^-16 relative, dropped).
+// Paired bf16x3 (x3_paired(KIND)): chunk k holds channels [16 k, 16 k + 16) as [hi | lo] 32-B halves
+// of every A row (source pieces 0-1 from the hi plane, 2-3 from the lo plane) and of every packed
+// weight row, and its three k-groups multiply halves (0, 0), (0, 1), (1, 0) (A half, B half).
 template <typename T, int KIND, int XS = 0>
 struct DmaPlan {
   using G = ConvGeom<T, KIND>;
+  static constexpr bool P3 = XS != 0 && x3_paired(KIND);
   static constexpr int X3 = XS ? 3 : 1, RS = XS ? 2 : 1;   // chunk multiplicity, row-stride factor
+  static constexpr int KCP = P3 ? G::KC / 2 : G::KC;      // channels per chunk (of one plane)
   i32x4 rs1, rs2, rsw;                // buffer resources: src1, src2, packed weights
   int nc1 = 0, nc2 = 0, cc1 = 0, cc2 = 0;   // XS: chunks per plane and channels of both segments
   int avoff1[G::APT], avoff2[G::APT]; // byte offsets of this lane's A pieces (chunk 0) in src1 / src2
@@ -524,8 +529,8 @@ struct DmaPlan {
   int n1, wv, wbase;                  // wbase: byte offset of this tile's chunk 0 in the packed weights
 
   __device__ __forceinline__ void init(const ConvArgs<T>& a, int m0, int n_tile, int NC, int wv_, int lane) {
-    n1 = X3 * (a.c1 / G::KC);
-    if constexpr (XS != 0) {
+    n1 = P3 ? a.c1 / KCP : X3 * (a.c1 / G::KC);
+    if constexpr (XS != 0 && !P3) {
       nc1 = a.c1 / G::KC;
       nc2 = a.c2 / G::KC;
       cc1 = a.c1;
@@ -552,8 +557,8 @@ struct DmaPlan {
       const int q1 = row / G::S;                 // fused: slot1 position index
       const int li = G::FUSED ? (q1 < G::LH ? 2 * q1 : 2 * (q1 - G::LH) + 1) : G::POSMAJ ? q1 : row - s * G::LIN;
       const int b = min(m0 + s, a.B - 1);        // rows of absent samples only feed unstored outputs
-      avoff1[qq] = ((b * G::LIN + li) * RS * a.c1 + c * G::EPC) * (int)sizeof(T);
-      avoff2[qq] = ((b * G::LIN + li) * RS * a.c2 + c * G::EPC) * (int)sizeof(T);
+      avoff1[qq] = ((b * G::LIN + li) * RS * a.c1 + pcol(c, a.c1)) * (int)sizeof(T);
+      avoff2[qq] = ((b * G::LIN + li) * RS * a.c2 + pcol(c, a.c2)) * (int)sizeof(T);
     }
     if constexpr (G::FUSED) {
 #pragma unroll
@@ -564,16 +569,24 @@ struct DmaPlan {
         const int c = cp ^ G::key(row);
         const int s = row % G::S, li = row / G::S;
         const int b = min(m0 + s, a.B - 1);
-        avoffh[qq] = ((b * G::LH + li) * RS * a.c2 + c * G::EPC) * (int)sizeof(T);
+        avoffh[qq] = ((b * G::LH + li) * RS * a.c2 + pcol(c, a.c2)) * (int)sizeof(T);
       }
     }
     bvoff = (wv * 64 + lane) * 16;
     wbase = n_tile * tile_bytes;
   }
 
+  // element offset within an input row of 16-B piece c of a chunk (paired: its half picks the plane
+  // of a row of C channels per plane)
+  static __device__ __forceinline__ int pcol(int c, int C) {
+    if constexpr (P3) return c < G::CPR / 2 ? c * G::EPC : C + (c - G::CPR / 2) * G::EPC;
+    else return c * G::EPC;
+  }
   // element offset within an input row of chunk k of a segment (nc chunks per plane, c channels)
   __device__ __forceinline__ int coff(int k, int nc, int c) const {
-    if constexpr (XS != 0) {
+    if constexpr (P3) {
+      return k * KCP;
+    } else if constexpr (XS != 0) {
       const int g = (k >= nc) + (k >= 2 * nc);        // 0: a_hi, 1: a_hi again, 2: a_lo
       return (k - g * nc) * G::KC + (g == 2 ? c : 0);
     } else {
@@ -1035,6 +1048,11 @@ struct SeamArgs {
   int prod_n = 0;            // producer N tiles
 };
 
+// byte offset (XOR) of the 32-B half of an A / B row that k-group g of a chunk reads: halves 0, 1
+// (bf16: the chunk's two 16-channel groups), or (paired bf16x3) A halves 0, 0, 1 and B halves 0, 1, 0
+template <bool P3> __device__ __forceinline__ constexpr int kg_a(int g) { return P3 ? (g == 2 ? 32 : 0) : g << 5; }
+template <bool P3> __device__ __forceinline__ constexpr int kg_b(int g) { return P3 ? (g == 1 ? 32 : 0) : g << 5; }
+
 template <typename T, int KIND, int XS, int SEAM>
 __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int bid, const SeamArgs sa) {
   using G = ConvGeom<T, KIND>;
@@ -1089,7 +1107,8 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
 #endif
   const int m0 = m_tile * G::S;
 
-  const int NC = (XS ? 3 : 1) * (a.c1 / G::KC + a.c2 / G::KC);
+  constexpr bool P3 = DmaPlan<T, KIND, XS>::P3;     // paired bf16x3 chunks (x3_paired)
+  const int NC = P3 ? (a.c1 + a.c2) / (G::KC / 2) : (XS ? 3 : 1) * (a.c1 / G::KC + a.c2 / G::KC);
 
   // Final level: this thread's output row (one per thread) and every global operand of its
   // p_sample, loaded at kernel start.  They are older than every LDS-DMA of the K loop, so the
@@ -1234,7 +1253,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   // (segment 1) or coarse row Q = i + k (segment 2) relative to its first fragment; each step
   // reads only the positions no earlier step of its k-group has read.  cav carries the last
   // step's A operands into the next chunk's first step (whose MFMAs they are).
-  constexpr bool REUSE = CONV_TAP_REUSE && G::FUSED && G::S == 32 && sizeof(T) == 2 && !G::ZS;
+  constexpr bool REUSE = CONV_TAP_REUSE && G::FUSED && G::S == 32 && sizeof(T) == 2 && !G::ZS && !P3;
   fragT cav[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) cav[i] = fragT{};
@@ -1253,7 +1272,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   for (int g = 0; g < NGE; ++g) epk[g][0] = epk[g][1] = fragT{};
   const char* ebase = nullptr;
   if constexpr (G::FUSED) {
-    const int n2 = (XS ? 3 : 1) * (a.c2 / G::KC);
+    const int n2 = P3 ? a.c2 / (G::KC / 2) : (XS ? 3 : 1) * (a.c2 / G::KC);
     ebase = reinterpret_cast<const char*>(a.epack) +
             ((size_t)n_tile * n2 * 2 * NT + (size_t)ph * NT + wn * 64 + lr) * ROWB + h * 16;
   }
@@ -1281,7 +1300,8 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       // segment-2 chunk (SEGV == 4: peeled at compile time; a runtime choice there made the compiler
       // shuffle the accumulators between two register assignments every chunk).
       constexpr int PAT = decltype(pat_tag)::value;
-      constexpr int NG = ROWB / 32;
+      constexpr int NG = P3 ? 3 : ROWB / 32;   // k-groups per chunk (paired bf16x3: 3)
+      constexpr int NH = ROWB / 32;             // 32-B halves of a row
       constexpr int NT_ = SEG == 2 ? G::TAPS2 : TAPS;
       constexpr int NS = NT_ * NG;
       constexpr int NPER = NEXT == 3 ? G::PER2 : G::PER;
@@ -1289,7 +1309,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       constexpr int PPS = (NPC + NS - 1) / NS;
       constexpr bool M0 = (PAT & 1) == 0;                 // fragment 0 is coarse row 0 (edge correction)
       static_assert(NS % 2 == 0, "fragment double buffer alternates per step");
-      fragT am[SEG == 2 ? NG : 1];
+      fragT am[SEG == 2 ? NH : 1];
       auto tap_of = [](int jj) { return SEG == 2 ? jj : (jj < 3 ? 2 * jj : 2 * (jj - 3) + 1); };
       auto ok = [](int i, int j) { return SEG == 2 ? G::zs_valid2(PAT, i, j) : G::zs_valid1(PAT, i, j); };
 #pragma unroll
@@ -1303,11 +1323,11 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         } else {
           ao0 = aoff[j][0]; ao1 = aoff[j][1]; ao2 = aoff[j][2]; bo0 = boff[0]; bo1 = boff[1];
         }
-        const char* pa0 = base + (ao0 ^ (g << 5));
-        const char* pa1 = base + (ao1 ^ (g << 5));
-        const char* pa2 = base + (ao2 ^ (g << 5));
-        const char* pb0 = base + ((bo0 + j * NT * ROWB) ^ (g << 5));
-        const char* pb1 = base + ((bo1 + j * NT * ROWB) ^ (g << 5));
+        const char* pa0 = base + (ao0 ^ kg_a<P3>(g));
+        const char* pa1 = base + (ao1 ^ kg_a<P3>(g));
+        const char* pa2 = base + (ao2 ^ kg_a<P3>(g));
+        const char* pb0 = base + ((bo0 + j * NT * ROWB) ^ kg_b<P3>(g));
+        const char* pb1 = base + ((bo1 + j * NT * ROWB) ^ kg_b<P3>(g));
         // the MFMAs of step st - 1 (fragment i, B half jn) and the reads of step st
         auto body = [&](auto prev_tag) {
           constexpr int PV = decltype(prev_tag)::value;   // 0: this segment's step st - 1; 1: segment 1's last; 2: segment 2's last
@@ -1347,14 +1367,14 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
           // at step 0, multiplied after step 0's MFMAs (issued at step 1); then the next chunk's weights
           if (st == 0) {
 #pragma unroll
-            for (int gg = 0; gg < NG; ++gg) am[gg] = *reinterpret_cast<const fragT*>(base + (amask ^ (gg << 5)));
+            for (int gg = 0; gg < NH; ++gg) am[gg] = *reinterpret_cast<const fragT*>(base + (amask ^ (gg << 5)));
           }
           if (st == 1) {
 #pragma unroll
             for (int gg = 0; gg < NG; ++gg)
 #pragma unroll
               for (int jn = 0; jn < 2; ++jn)
-                if constexpr (!(CONV_EXP_MODE & 2)) acc[0][jn] = mfma32(am[gg], epk[gg][jn], acc[0][jn]);
+                if constexpr (!(CONV_EXP_MODE & 2)) acc[0][jn] = mfma32(am[kg_a<P3>(gg) >> 5], epk[kg_b<P3>(gg) >> 5][jn], acc[0][jn]);
             const int k2 = kc - dma.n1;
             if (kc + 1 < NC) load_epk(k2 + 1);
           }
@@ -1507,7 +1527,8 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     } else if constexpr (G::PM) {
       // position-major down3: step st = (tap j, k-group g); the MFMAs of step st - 1 and the reads
       // of step st, both over this wave's valid fragments only (pm_valid folds after unrolling)
-      constexpr int NG = ROWB / 32;
+      constexpr int NG = P3 ? 3 : ROWB / 32;   // k-groups per chunk (paired bf16x3: 3)
+      constexpr int NH = ROWB / 32;             // 32-B halves of a row
       constexpr int NS = TAPS * NG;
       constexpr int NPER = G::PER;
       constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;
@@ -1519,11 +1540,11 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         for (int st = 0; st < NS; ++st) {
           const int j = st / NG, g = st % NG, sb = st & 1, pb = sb ^ 1;
           const int jp = st == 0 ? TAPS - 1 : (st - 1) / NG;   // st = 0: the previous chunk's last step
-          const char* pa0 = base + (aoff[j][0] ^ (g << 5));
-          const char* pa1 = base + (aoff[j][1] ^ (g << 5));
-          const char* pa2 = base + (aoff[j][2] ^ (g << 5));
-          const char* pb0 = base + ((boff[0] + j * NT * ROWB) ^ (g << 5));
-          const char* pb1 = base + ((boff[1] + j * NT * ROWB) ^ (g << 5));
+          const char* pa0 = base + (aoff[j][0] ^ kg_a<P3>(g));
+          const char* pa1 = base + (aoff[j][1] ^ kg_a<P3>(g));
+          const char* pa2 = base + (aoff[j][2] ^ kg_a<P3>(g));
+          const char* pb0 = base + ((boff[0] + j * NT * ROWB) ^ kg_b<P3>(g));
+          const char* pb1 = base + ((boff[1] + j * NT * ROWB) ^ kg_b<P3>(g));
 #define PETDIFF_PMF(i, jn)                                                                                 \
   if (G::pm_valid(PAT, i, jp)) {                                                                           \
     if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(av[pb][i], bv[pb][jn], acc[i][jn]);            \
@@ -1560,7 +1581,8 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         }
       }
     } else if constexpr (sizeof(T) == 2) {
-      constexpr int NG = ROWB / 32;
+      constexpr int NG = P3 ? 3 : ROWB / 32;   // k-groups per chunk (paired bf16x3: 3)
+      constexpr int NH = ROWB / 32;             // 32-B halves of a row
       constexpr int NT_ = SEG == 2 ? G::TAPS2 : TAPS;
       constexpr int NS = NT_ * NG;
       // NEXT: 0 none, 1 the next chunk, 2 the next two chunks, 3 the next chunk, a fused segment-2 one
@@ -1568,7 +1590,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;     // pieces to issue over this chunk
       constexpr int PPS = (NPC + NS - 1) / NS;            // DMA pieces per step
       static_assert(NS % 2 == 0, "fragment double buffer alternates per step");
-      fragT am[SEG == 2 ? NG : 1];
+      fragT am[SEG == 2 ? NH : 1];
 #pragma unroll
       for (int st = 0; st < NS; ++st) {
         const int j = st / NG, g = st % NG, sb = st & 1;
@@ -1580,11 +1602,11 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         } else {
           ao0 = aoff[j][0]; ao1 = aoff[j][1]; ao2 = aoff[j][2]; bo0 = boff[0]; bo1 = boff[1];
         }
-        const char* pa0 = base + (ao0 ^ (g << 5));
-        const char* pa1 = base + (ao1 ^ (g << 5));
-        const char* pa2 = base + (ao2 ^ (g << 5));
-        const char* pb0 = base + ((bo0 + j * NT * ROWB) ^ (g << 5));
-        const char* pb1 = base + ((bo1 + j * NT * ROWB) ^ (g << 5));
+        const char* pa0 = base + (ao0 ^ kg_a<P3>(g));
+        const char* pa1 = base + (ao1 ^ kg_a<P3>(g));
+        const char* pa2 = base + (ao2 ^ kg_a<P3>(g));
+        const char* pb0 = base + ((bo0 + j * NT * ROWB) ^ kg_b<P3>(g));
+        const char* pb1 = base + ((bo1 + j * NT * ROWB) ^ kg_b<P3>(g));
         const int pb = sb ^ 1;
 #define PETDIFF_MF(i, jn)                                                                                  \
   if constexpr (!(CONV_EXP_MODE & 2))                                                                      \
@@ -1614,14 +1636,14 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
           // after step 0's reads, multiplied after step 1's MFMAs; then the next chunk's weights
           if (st == 0 && has_m0) {
 #pragma unroll
-            for (int gg = 0; gg < NG; ++gg) am[gg] = *reinterpret_cast<const fragT*>(base + (amask ^ (gg << 5)));
+            for (int gg = 0; gg < NH; ++gg) am[gg] = *reinterpret_cast<const fragT*>(base + (amask ^ (gg << 5)));
           }
           if (st == 1 && has_m0) {
 #pragma unroll
             for (int gg = 0; gg < NG; ++gg)
 #pragma unroll
               for (int jn = 0; jn < 2; ++jn)
-                if constexpr (!(CONV_EXP_MODE & 2)) acc[0][jn] = mfma32(am[gg], epk[gg][jn], acc[0][jn]);
+                if constexpr (!(CONV_EXP_MODE & 2)) acc[0][jn] = mfma32(am[kg_a<P3>(gg) >> 5], epk[kg_b<P3>(gg) >> 5][jn], acc[0][jn]);
             const int k2 = kc - dma.n1;
             if (kc + 1 < NC) load_epk(k2 + 1);
           }
