@@ -120,6 +120,28 @@
 #define CONV_UP0_ZS 1
 #endif
 
+// Issue order of a step's 6 MFMAs (fragment i, B half jn): 0 = A-major (0,0) (0,1) (1,0) (1,1) (2,0)
+// (2,1), the reads interleaved a0 b0 b1 a1 a2; 1 = B-major (0,0) (1,0) (2,0) (0,1) (1,1) (2,1), consecutive
+// MFMAs sharing their B operand, the reads a0 b0 a1 a2 b1 (in the order the next step consumes them).
+// Each accumulator still takes its MFMAs in step order, so the results are bitwise the same.
+// Measured (profiles/r03/ab/mfma_order): up2.fused 38.3-38.4 vs 39.1-39.4 us in conv_micro, the other
+// layers within noise, bench 5062-5122 vs 5045-5111 samples/s; kept.
+#ifndef CONV_MFMA_ORDER
+#define CONV_MFMA_ORDER 1
+#endif
+#define PETDIFF_CALL(m, a) m a
+#if CONV_MFMA_ORDER
+#define PETDIFF_O1 (1, 0)
+#define PETDIFF_O2 (2, 0)
+#define PETDIFF_O3 (0, 1)
+#define PETDIFF_O4 (1, 1)
+#else
+#define PETDIFF_O1 (0, 1)
+#define PETDIFF_O2 (1, 0)
+#define PETDIFF_O3 (1, 1)
+#define PETDIFF_O4 (2, 0)
+#endif
+
 namespace petdiff {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -1343,17 +1365,27 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
           PETDIFF_ZMF(0, 0)
           PETDIFF_ZRD(av[sb][0], pa0, ok(0, j))
           __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_ZMF(0, 1)
+          PETDIFF_CALL(PETDIFF_ZMF, PETDIFF_O1)
           PETDIFF_ZRD(bv[sb][0], pb0, true)
           __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_ZMF(1, 0)
-          PETDIFF_ZRD(bv[sb][1], pb1, true)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_ZMF(1, 1)
+          PETDIFF_CALL(PETDIFF_ZMF, PETDIFF_O2)
+#if CONV_MFMA_ORDER
           PETDIFF_ZRD(av[sb][1], pa1, ok(1, j))
           __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_ZMF(2, 0)
+          PETDIFF_CALL(PETDIFF_ZMF, PETDIFF_O3)
           PETDIFF_ZRD(av[sb][2], pa2, ok(2, j))
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_CALL(PETDIFF_ZMF, PETDIFF_O4)
+          PETDIFF_ZRD(bv[sb][1], pb1, true)
+#else
+          PETDIFF_ZRD(bv[sb][1], pb1, true)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_CALL(PETDIFF_ZMF, PETDIFF_O3)
+          PETDIFF_ZRD(av[sb][1], pa1, ok(1, j))
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_CALL(PETDIFF_ZMF, PETDIFF_O4)
+          PETDIFF_ZRD(av[sb][2], pa2, ok(2, j))
+#endif
           __builtin_amdgcn_sched_barrier(0);
           PETDIFF_ZMF(2, 1)
 #undef PETDIFF_ZRD
@@ -1554,17 +1586,27 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
           PETDIFF_PMF(0, 0)
           PETDIFF_PRD(av[sb][0], pa0, G::pm_valid(PAT, 0, j))
           __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_PMF(0, 1)
+          PETDIFF_CALL(PETDIFF_PMF, PETDIFF_O1)
           PETDIFF_PRD(bv[sb][0], pb0, true)
           __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_PMF(1, 0)
-          PETDIFF_PRD(bv[sb][1], pb1, true)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_PMF(1, 1)
+          PETDIFF_CALL(PETDIFF_PMF, PETDIFF_O2)
+#if CONV_MFMA_ORDER
           PETDIFF_PRD(av[sb][1], pa1, G::pm_valid(PAT, 1, j))
           __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_PMF(2, 0)
+          PETDIFF_CALL(PETDIFF_PMF, PETDIFF_O3)
           PETDIFF_PRD(av[sb][2], pa2, G::pm_valid(PAT, 2, j))
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_CALL(PETDIFF_PMF, PETDIFF_O4)
+          PETDIFF_PRD(bv[sb][1], pb1, true)
+#else
+          PETDIFF_PRD(bv[sb][1], pb1, true)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_CALL(PETDIFF_PMF, PETDIFF_O3)
+          PETDIFF_PRD(av[sb][1], pa1, G::pm_valid(PAT, 1, j))
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_CALL(PETDIFF_PMF, PETDIFF_O4)
+          PETDIFF_PRD(av[sb][2], pa2, G::pm_valid(PAT, 2, j))
+#endif
           __builtin_amdgcn_sched_barrier(0);
           PETDIFF_PMF(2, 1)
 #undef PETDIFF_PRD
@@ -1616,17 +1658,27 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         PETDIFF_MF(0, 0)
         PETDIFF_RD(av[sb][0], pa0)
         __builtin_amdgcn_sched_barrier(0);
-        PETDIFF_MF(0, 1)
+        PETDIFF_CALL(PETDIFF_MF, PETDIFF_O1)
         PETDIFF_RD(bv[sb][0], pb0)
         __builtin_amdgcn_sched_barrier(0);
-        PETDIFF_MF(1, 0)
-        PETDIFF_RD(bv[sb][1], pb1)
-        __builtin_amdgcn_sched_barrier(0);
-        PETDIFF_MF(1, 1)
+        PETDIFF_CALL(PETDIFF_MF, PETDIFF_O2)
+#if CONV_MFMA_ORDER
         PETDIFF_RD(av[sb][1], pa1)
         __builtin_amdgcn_sched_barrier(0);
-        PETDIFF_MF(2, 0)
+        PETDIFF_CALL(PETDIFF_MF, PETDIFF_O3)
         PETDIFF_RD(av[sb][2], pa2)
+        __builtin_amdgcn_sched_barrier(0);
+        PETDIFF_CALL(PETDIFF_MF, PETDIFF_O4)
+        PETDIFF_RD(bv[sb][1], pb1)
+#else
+        PETDIFF_RD(bv[sb][1], pb1)
+        __builtin_amdgcn_sched_barrier(0);
+        PETDIFF_CALL(PETDIFF_MF, PETDIFF_O3)
+        PETDIFF_RD(av[sb][1], pa1)
+        __builtin_amdgcn_sched_barrier(0);
+        PETDIFF_CALL(PETDIFF_MF, PETDIFF_O4)
+        PETDIFF_RD(av[sb][2], pa2)
+#endif
         __builtin_amdgcn_sched_barrier(0);
         PETDIFF_MF(2, 1)
 #undef PETDIFF_RD
