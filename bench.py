@@ -31,10 +31,12 @@ FLOP_PER_SAMPLE_STEP = 296_361_984          # x-dependent U-Net convs incl. 1x1 
 UP0_BLOCK_FLOP_PER_SAMPLE = 2 * 12 * 512 * 1024 * 7
 UP0_BLOCK_EXEC_FLOP_PER_SAMPLE = 2 * 12 * 512 * 1024 * 6   # executed (residual folded into the centre tap)
 # fused up0 level (16-bit default): up0's k2 conv (App. A: 13.20 M MAC, 1074 input channels) + the block
-# in one kernel; executed = skip half (6 taps x 512) + 2-phase composite (4 taps x 1024) + the l = 0, 1
-# left-edge correction rows (1024 -> 512 each)
+# in one kernel; executed = skip half (6 taps x 512 at 12 positions) + 2-phase composite (4 taps x 1024 at
+# 6 coarse rows per phase) + the l = 0, 1 left-edge correction rows (1024 -> 512 each), less the (position,
+# tap) products that read only padding, which the kernel skips (CONV_UP0_ZS): 63 of the 72 skip-half
+# products and 20 of the 24 composite products per phase remain
 UP0_CONV2_FLOP_PER_SAMPLE = 2 * 12 * 2 * 1074 * 512
-UP0_FUSED_EXEC_FLOP_PER_SAMPLE = 2 * 12 * 512 * 512 * 6 + 2 * 12 * 4 * 1024 * 512 + 2 * 2 * 1024 * 512
+UP0_FUSED_EXEC_FLOP_PER_SAMPLE = 2 * 512 * 512 * 63 + 2 * 2 * 1024 * 512 * 20 + 2 * 2 * 1024 * 512
 PEAK_BF16_TFLOPS = 2500.0                   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0                       # HBM3E (MI355X_MICROARCH.md)
