@@ -1560,7 +1560,6 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       // position-major down3: step st = (tap j, k-group g); the MFMAs of step st - 1 and the reads
       // of step st, both over this wave's valid fragments only (pm_valid folds after unrolling)
       constexpr int NG = P3 ? 3 : ROWB / 32;   // k-groups per chunk (paired bf16x3: 3)
-      constexpr int NH = ROWB / 32;             // 32-B halves of a row
       constexpr int NS = TAPS * NG;
       constexpr int NPER = G::PER;
       constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;
