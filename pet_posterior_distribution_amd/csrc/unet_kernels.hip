@@ -119,6 +119,20 @@
 #ifndef CONV_UP0_ZS
 #define CONV_UP0_ZS 1
 #endif
+// up0 zero-skip with the A fragments cached per input position: within a k-group each position a wave's
+// (fragment, tap) pairs read is loaded from LDS once (the taps of neighbouring fragments overlap), and a
+// paired bf16x3 chunk's (a_hi, w_lo) group reuses its (a_hi, w_hi) group's A fragments.  The LDS fragment
+// reads cost the chip about as much power as the L2 -> LDS stream (conv_micro stamps: 1.95 GHz without
+// either, 1.6 with both).  0 = one read per (fragment, tap).
+#ifndef CONV_UP0_ZS_CACHE
+#define CONV_UP0_ZS_CACHE 1
+#endif
+// The same per-position A cache on the position-major down layers (down2, down3), whose fragments are also
+// one position of 32 samples: a fragment set's taps read 6-12 distinct positions instead of 13-16 (fragment,
+// tap) pairs per k-group.
+#ifndef CONV_PM_CACHE
+#define CONV_PM_CACHE 1
+#endif
 
 // Issue order of a step's 6 MFMAs (fragment i, B half jn): 0 = A-major (0,0) (0,1) (1,0) (1,1) (2,0)
 // (2,1), the reads interleaved a0 b0 b1 a1 a2; 1 = B-major (0,0) (1,0) (2,0) (0,1) (1,1) (2,1), consecutive
@@ -345,6 +359,13 @@ struct ConvGeom {
   static constexpr __device__ __host__ bool pm_valid(int pat, int i, int j) {
     return pm_pos(pat, i) + j - PADL >= 0 && pm_pos(pat, i) + j - PADL < L;
   }
+  // (fragment i, tap j) is the first pair of set pat, in tap order, to read its input position
+  static constexpr __device__ __host__ bool pm_first(int pat, int i, int j) {
+    for (int j2 = 0; j2 < j; ++j2)
+      for (int i2 = 0; i2 < 3; ++i2)
+        if (pm_valid(pat, i2, j2) && pm_pos(pat, i2) + j2 == pm_pos(pat, i) + j) return false;
+    return true;
+  }
   // position -> 3 pat + i (the inverse table)
   static constexpr unsigned long long pm_inv_tab() {
     unsigned long long t = 0;
@@ -400,6 +421,25 @@ struct ConvGeom {
   }
   static constexpr __device__ __host__ bool zs_valid2(int pat, int i, int k) {
     return zs_m(pat & 1, i) - 1 + k >= 0 && zs_m(pat & 1, i) - 1 + k < LH;
+  }
+  // segment seg's tap order (segment 1: 0 2 4 1 3 5), the input position (fine l or coarse q) that
+  // fragment i of wave pat reads at tap j, and whether tap order index jj is the first in a k-group to read it
+  static constexpr __device__ __host__ int zs_tap(int seg, int jj) {
+    return seg == 2 ? jj : (jj < 3 ? 2 * jj : 2 * (jj - 3) + 1);
+  }
+  static constexpr __device__ __host__ int zs_pos(int seg, int pat, int i, int j) {
+    return seg == 2 ? zs_m(pat & 1, i) - 1 + j : 2 * zs_m(pat & 1, i) + (pat >> 1) + j - PADL;
+  }
+  static constexpr __device__ __host__ bool zs_ok(int seg, int pat, int i, int j) {
+    return seg == 2 ? zs_valid2(pat, i, j) : zs_valid1(pat, i, j);
+  }
+  static constexpr __device__ __host__ bool zs_first(int seg, int pat, int i, int jj) {
+    for (int j2 = 0; j2 < jj; ++j2)
+      for (int i2 = 0; i2 < 3; ++i2)
+        if (zs_ok(seg, pat, i2, zs_tap(seg, j2)) &&
+            zs_pos(seg, pat, i2, zs_tap(seg, j2)) == zs_pos(seg, pat, i, zs_tap(seg, jj)))
+          return false;
+    return true;
   }
   // first tile row of wave wm's fragment i (tile rows stay [phase][m][sample] for the epilogue)
   static __device__ __forceinline__ int frag_row(int wm, int i) {
@@ -1267,8 +1307,8 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   if constexpr ((CONV_EXP_MODE & 64) != 0) {   // diagnostic: non-zero register operands
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      av[0][0][e] = av[1][1][e] = av[0][2][e] = (decltype(av[0][0][0]))(0.01f * (lane + e));
-      bv[0][1][e] = bv[1][0][e] = (decltype(bv[0][0][0]))(0.02f * (lane - e));
+      av[0][0][e] = av[1][1][e] = av[0][2][e] = (std::remove_reference_t<decltype(av[0][0][0])>)(0.01f * (lane + e));
+      bv[0][1][e] = bv[1][0][e] = (std::remove_reference_t<decltype(bv[0][0][0])>)(0.02f * (lane - e));
     }
   }
   // Tap reuse (CONV_TAP_REUSE): this wave's fragment i at tap j reads fine position P = 2i + j
@@ -1279,6 +1319,14 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   fragT cav[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) cav[i] = fragT{};
+  // up0 zero-skip with cached A fragments: [32-B half][input position] (CONV_UP0_ZS_CACHE)
+  constexpr bool ZAP = (G::ZS && CONV_UP0_ZS_CACHE) || (G::PM && CONV_PM_CACHE);
+  constexpr int ZAP_H = ZAP ? 2 : 1, ZAP_P = ZAP ? G::L : 1;
+  fragT zap[ZAP_H][ZAP_P];
+#pragma unroll
+  for (int hh = 0; hh < ZAP_H; ++hh)
+#pragma unroll
+    for (int p = 0; p < ZAP_P; ++p) zap[hh][p] = fragT{};
   auto mfma_bf16 = [&](int pb) {
 #pragma unroll
     for (int i = 0; i < 3; ++i)
@@ -1315,7 +1363,111 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     constexpr int SEGV = (int)decltype(seg_tag)::value;
     constexpr int SEG = SEGV == 4 ? 2 : SEGV;
     char* nbase = smem + nbuf * G::STAGE;
-    if constexpr (G::ZS) {
+    if constexpr (G::ZS && CONV_UP0_ZS_CACHE) {
+      // up0 zero-skip, A fragments cached per position (zap[half][position]): step st = (k-group g, tap
+      // zs_tap(jj)); the reads of step st are B and the positions first needed at this tap in this half,
+      // the MFMAs of step st - 1 take their A operand from zap.  zap[h] is rewritten only by a later chunk's
+      // group of the same half, after every MFMA of this chunk's group has been issued (the carried last
+      // step at st = 0 reads the last group's half, never half 0).
+      constexpr int PAT = decltype(pat_tag)::value;
+      constexpr int NG = P3 ? 3 : ROWB / 32;
+      constexpr int NH = ROWB / 32;
+      constexpr int NT_ = SEG == 2 ? G::TAPS2 : TAPS;
+      constexpr int NS = NT_ * NG;
+      constexpr int NPER = NEXT == 3 ? G::PER2 : G::PER;
+      constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;
+      constexpr int PPS = (NPC + NS - 1) / NS;
+      constexpr bool M0 = (PAT & 1) == 0;
+      constexpr int HL = kg_a<P3>(NG - 1) >> 5;           // half of the last group (carried into st = 0)
+      static_assert(NS % 2 == 0 && HL != 0, "B double buffer alternates per step; carried half");
+      fragT am[SEG == 2 ? NH : 1];
+#pragma unroll
+      for (int st = 0; st < NS; ++st) {
+        const int g = st / NT_, jj = st % NT_, sb = st & 1, pb = sb ^ 1;
+        const int j = G::zs_tap(SEG, jj);
+        const int ah = kg_a<P3>(g) >> 5;
+        const bool fg = !P3 || g != 1;                    // the first group of its A half reads A
+        const int gp = st == 0 ? NG - 1 : (st - 1) / NT_;
+        const int jpp = G::zs_tap(SEG, (st == 0 ? NS - 1 : st - 1) % NT_);
+        const int ahp = kg_a<P3>(gp) >> 5;
+        int ao0, ao1, ao2, bo0, bo1;
+        if constexpr (SEG == 2) {
+          ao0 = aoff2[j][0]; ao1 = aoff2[j][1]; ao2 = aoff2[j][2]; bo0 = boff2[0]; bo1 = boff2[1];
+        } else {
+          ao0 = aoff[j][0]; ao1 = aoff[j][1]; ao2 = aoff[j][2]; bo0 = boff[0]; bo1 = boff[1];
+        }
+        const char* pa0 = base + (ao0 ^ kg_a<P3>(g));
+        const char* pa1 = base + (ao1 ^ kg_a<P3>(g));
+        const char* pa2 = base + (ao2 ^ kg_a<P3>(g));
+        const char* pb0 = base + ((bo0 + j * NT * ROWB) ^ kg_b<P3>(g));
+        const char* pb1 = base + ((bo1 + j * NT * ROWB) ^ kg_b<P3>(g));
+        auto rdA = [&](int i) { return fg && G::zs_ok(SEG, PAT, i, j) && G::zs_first(SEG, PAT, i, jj); };
+        auto body = [&](auto prev_tag) {
+          constexpr int PV = decltype(prev_tag)::value;   // 0: this segment's step st - 1; 1 / 2: segment 1's / 2's last
+          constexpr int SP = PV == 0 ? SEG : PV;            // segment of the MFMAs' step
+          auto okp = [&](int i) { return G::zs_ok(SP, PAT, i, PV == 0 ? jpp : SP == 2 ? G::TAPS2 - 1 : TAPS - 1); };
+          auto posp = [&](int i) { return G::zs_pos(SP, PAT, i, PV == 0 ? jpp : SP == 2 ? G::TAPS2 - 1 : TAPS - 1); };
+#define PETDIFF_ZMF(i, jn)                                                                                 \
+  if (okp(i)) {                                                                                            \
+    if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(zap[ahp][posp(i)], bv[pb][jn], acc[i][jn]);     \
+  }
+#define PETDIFF_ZRA(i, ptr) \
+  if (rdA(i)) { if constexpr (!(CONV_EXP_MODE & 64)) zap[ah][G::zs_pos(SEG, PAT, i, j)] = *reinterpret_cast<const fragT*>(ptr); }
+#define PETDIFF_ZRB(dst, ptr) \
+  if constexpr (!(CONV_EXP_MODE & 64)) dst = *reinterpret_cast<const fragT*>(ptr);
+          PETDIFF_ZMF(0, 0)
+          PETDIFF_ZRA(0, pa0)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_ZMF(1, 0)
+          PETDIFF_ZRB(bv[sb][0], pb0)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_ZMF(2, 0)
+          PETDIFF_ZRA(1, pa1)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_ZMF(0, 1)
+          PETDIFF_ZRA(2, pa2)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_ZMF(1, 1)
+          PETDIFF_ZRB(bv[sb][1], pb1)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_ZMF(2, 1)
+#undef PETDIFF_ZRB
+#undef PETDIFF_ZRA
+#undef PETDIFF_ZMF
+        };
+        if (st > 0) body(std::integral_constant<int, 0>{});
+        else if constexpr (SEG == 1 || SEGV == 4) body(std::integral_constant<int, 1>{});
+        else body(std::integral_constant<int, 2>{});
+        if constexpr (SEG == 2 && M0) {
+          if (st == 0) {
+#pragma unroll
+            for (int gg = 0; gg < NH; ++gg) am[gg] = *reinterpret_cast<const fragT*>(base + (amask ^ (gg << 5)));
+          }
+          if (st == 1) {
+#pragma unroll
+            for (int gg = 0; gg < NG; ++gg)
+#pragma unroll
+              for (int jn = 0; jn < 2; ++jn)
+                if constexpr (!(CONV_EXP_MODE & 2)) acc[0][jn] = mfma32(am[kg_a<P3>(gg) >> 5], epk[kg_b<P3>(gg) >> 5][jn], acc[0][jn]);
+            const int k2 = kc - dma.n1;
+            if (kc + 1 < NC) load_epk(k2 + 1);
+          }
+        }
+        if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
+#pragma unroll
+          for (int u = 0; u < PPS; ++u) {
+            const int k = st * PPS + u;
+            if (k < NPER) {
+              if constexpr (NEXT == 3) dma.piece2(nbase, k, nkc - dma.n1, lane);
+              else dma.piece1(nbase, k, nkc, lane);
+            } else if (NEXT == 2 && k < NPC) {
+              dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else if constexpr (G::ZS) {
       // up0 zero-skip: step st = (k-group g, tap tap_of(jj)) in the tap-reuse path's order; the MFMAs
       // of step st - 1 and the reads of step st, both over the (fragment, tap) pairs that read data.
       // At st = 0 the MFMAs are the previous chunk's last step, of segment 1 when this is the first
@@ -1555,6 +1707,72 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         constexpr int jl = SEG == 2 ? NT_ - 1 : TAPS - 1;   // the last step's tap (order ends on 5 / 3)
 #pragma unroll
         for (int i = 0; i < 3; ++i) cav[i] = AP[NG - 1][jl + D * i];
+      }
+    } else if constexpr (G::PM && CONV_PM_CACHE) {
+      // position-major, A fragments cached per input position (zap[half][position], CONV_PM_CACHE): step
+      // st = (tap j, k-group g); the reads of step st are B and the positions that this set first needs at
+      // tap j (in the first group of their half), the MFMAs of step st - 1 take A from zap.  A position is
+      // rewritten only by the next chunk's first use of its half, after this chunk's last MFMA on it.
+      constexpr int NG = P3 ? 3 : ROWB / 32;
+      constexpr int NS = TAPS * NG;
+      constexpr int NPER = G::PER;
+      constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;
+      constexpr int PPS = (NPC + NS - 1) / NS;
+      static_assert(NS % 2 == 0 && (kg_a<P3>(NG - 1) >> 5) != 0, "B double buffer alternates per step; carried half");
+      {
+        constexpr int PAT = decltype(pat_tag)::value;
+#pragma unroll
+        for (int st = 0; st < NS; ++st) {
+          const int j = st / NG, g = st % NG, sb = st & 1, pb = sb ^ 1;
+          const int jp = st == 0 ? TAPS - 1 : (st - 1) / NG;
+          const int gp = st == 0 ? NG - 1 : (st - 1) % NG;
+          const int ah = kg_a<P3>(g) >> 5, ahp = kg_a<P3>(gp) >> 5;
+          const bool fg = !P3 || g != 1;                  // the first group of its A half reads A
+          const char* pa0 = base + (aoff[j][0] ^ kg_a<P3>(g));
+          const char* pa1 = base + (aoff[j][1] ^ kg_a<P3>(g));
+          const char* pa2 = base + (aoff[j][2] ^ kg_a<P3>(g));
+          const char* pb0 = base + ((boff[0] + j * NT * ROWB) ^ kg_b<P3>(g));
+          const char* pb1 = base + ((boff[1] + j * NT * ROWB) ^ kg_b<P3>(g));
+#define PETDIFF_CMF(i, jn)                                                                                  \
+  if (G::pm_valid(PAT, i, jp)) {                                                                            \
+    if constexpr (!(CONV_EXP_MODE & 2))                                                                     \
+      acc[i][jn] = mfma32(zap[ahp][G::pm_pos(PAT, i) + jp - PADL], bv[pb][jn], acc[i][jn]);                  \
+  }
+#define PETDIFF_CRA(i, ptr)                                                                                 \
+  if (fg && G::pm_valid(PAT, i, j) && G::pm_first(PAT, i, j)) {                                             \
+    if constexpr (!(CONV_EXP_MODE & 64)) zap[ah][G::pm_pos(PAT, i) + j - PADL] = *reinterpret_cast<const fragT*>(ptr); \
+  }
+#define PETDIFF_CRB(dst, ptr) \
+  if constexpr (!(CONV_EXP_MODE & 64)) dst = *reinterpret_cast<const fragT*>(ptr);
+          PETDIFF_CMF(0, 0)
+          PETDIFF_CRA(0, pa0)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_CMF(1, 0)
+          PETDIFF_CRB(bv[sb][0], pb0)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_CMF(2, 0)
+          PETDIFF_CRA(1, pa1)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_CMF(0, 1)
+          PETDIFF_CRA(2, pa2)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_CMF(1, 1)
+          PETDIFF_CRB(bv[sb][1], pb1)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_CMF(2, 1)
+#undef PETDIFF_CRB
+#undef PETDIFF_CRA
+#undef PETDIFF_CMF
+          if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
+#pragma unroll
+            for (int u = 0; u < PPS; ++u) {
+              const int k = st * PPS + u;
+              if (k < NPER) dma.piece1(nbase, k, nkc, lane);
+              else if (NEXT == 2 && k < NPC) dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
     } else if constexpr (G::PM) {
       // position-major down3: step st = (tap j, k-group g); the MFMAs of step st - 1 and the reads
@@ -1946,12 +2164,18 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         ring_barrier<0>();
         if constexpr (G::ZS) {   // the last chunk's last step (composite tap 3) over this set's valid fragments
           constexpr int PAT = decltype(pat_tag)::value;
+          constexpr int HL = kg_a<P3>((P3 ? 3 : ROWB / 32) - 1) >> 5;
 #pragma unroll
           for (int i = 0; i < 3; ++i)
             if (G::zs_valid2(PAT, i, G::TAPS2 - 1))
 #pragma unroll
               for (int jn = 0; jn < 2; ++jn)
-                if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(av[1][i], bv[1][jn], acc[i][jn]);
+                if constexpr (!(CONV_EXP_MODE & 2)) {
+                  if constexpr (CONV_UP0_ZS_CACHE)
+                    acc[i][jn] = mfma32(zap[HL][G::zs_pos(2, PAT, i, G::TAPS2 - 1)], bv[1][jn], acc[i][jn]);
+                  else
+                    acc[i][jn] = mfma32(av[1][i], bv[1][jn], acc[i][jn]);
+                }
         }
       };
       // up0 zero-skip: each wave's fragment set gets its own main loop (no per-step branch)
@@ -2058,12 +2282,18 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         }
         if constexpr (G::PM) {   // the last step (tap TAPS - 1) of this wave's valid fragments
           constexpr int PAT = decltype(pat_tag)::value;
+          constexpr int HL = kg_a<P3>((P3 ? 3 : ROWB / 32) - 1) >> 5;
 #pragma unroll
           for (int i = 0; i < 3; ++i)
             if (G::pm_valid(PAT, i, TAPS - 1))
 #pragma unroll
               for (int jn = 0; jn < 2; ++jn)
-                if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(av[1][i], bv[1][jn], acc[i][jn]);
+                if constexpr (!(CONV_EXP_MODE & 2)) {
+                  if constexpr (CONV_PM_CACHE)
+                    acc[i][jn] = mfma32(zap[HL][G::pm_pos(PAT, i) + TAPS - 1 - PADL], bv[1][jn], acc[i][jn]);
+                  else
+                    acc[i][jn] = mfma32(av[1][i], bv[1][jn], acc[i][jn]);
+                }
         }
       };
       // position-major: each fragment set gets its own main loop (no per-chunk branch)
