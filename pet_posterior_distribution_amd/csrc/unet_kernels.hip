@@ -127,6 +127,13 @@
 #ifndef CONV_UP0_ZS_CACHE
 #define CONV_UP0_ZS_CACHE 1
 #endif
+// up0 zero-skip with 6 fragments per wave: wave w computes phase w >> 1, all 6 coarse rows (192 tile rows),
+// for output columns [32 (w & 1), +32) -- one B fragment per step for 6 MFMAs instead of two for 6, and with
+// the per-position cache 12 (6) A reads per segment-1 (-2) k-group.  LDS fragment reads per MFMA drop about
+// a quarter; the zero products per wave stay balanced (phase 0: 32 / 21, phase 1: 31 / 21 per k-group).
+#ifndef CONV_UP0_W6
+#define CONV_UP0_W6 1
+#endif
 // The same per-position A cache on the position-major down layers (down2, down3), whose fragments are also
 // one position of 32 samples: a fragment set's taps read 6-12 distinct positions instead of 13-16 (fragment,
 // tap) pairs per k-group.
@@ -438,6 +445,21 @@ struct ConvGeom {
       for (int i2 = 0; i2 < 3; ++i2)
         if (zs_ok(seg, pat, i2, zs_tap(seg, j2)) &&
             zs_pos(seg, pat, i2, zs_tap(seg, j2)) == zs_pos(seg, pat, i, zs_tap(seg, jj)))
+          return false;
+    return true;
+  }
+  // CONV_UP0_W6: fragment f (0..5) of a phase-e wave is coarse row m = f
+  static constexpr bool W6 = ZS && CONV_UP0_ZS_CACHE && CONV_UP0_W6;
+  static constexpr __device__ __host__ int w6_pos(int seg, int e, int f, int j) {
+    return seg == 2 ? f - 1 + j : 2 * f + e + j - PADL;
+  }
+  static constexpr __device__ __host__ bool w6_ok(int seg, int e, int f, int j) {
+    return w6_pos(seg, e, f, j) >= 0 && w6_pos(seg, e, f, j) < (seg == 2 ? LH : L);
+  }
+  static constexpr __device__ __host__ bool w6_first(int seg, int e, int f, int jj) {
+    for (int j2 = 0; j2 < jj; ++j2)
+      for (int f2 = 0; f2 < 6; ++f2)
+        if (w6_ok(seg, e, f2, zs_tap(seg, j2)) && w6_pos(seg, e, f2, zs_tap(seg, j2)) == w6_pos(seg, e, f, zs_tap(seg, jj)))
           return false;
     return true;
   }
@@ -1110,6 +1132,17 @@ struct SeamArgs {
   int prod_n = 0;            // producer N tiles
 };
 
+// compile-time loop: f(integral_constant<int, I>) for I in [I0, N) (the step index of a fully unrolled main
+// loop whose register-array indices must fold; a #pragma unroll the compiler declines leaves them dynamic,
+// i.e. in scratch)
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
 // byte offset (XOR) of the 32-B half of an A / B row that k-group g of a chunk reads: halves 0, 1
 // (bf16: the chunk's two 16-channel groups), or (paired bf16x3) A halves 0, 0, 1 and B halves 0, 1, 0
 template <bool P3> __device__ __forceinline__ constexpr int kg_a(int g) { return P3 ? (g == 2 ? 32 : 0) : g << 5; }
@@ -1253,8 +1286,8 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   // left-edge correction (amask: coarse row 0, registers epk), only in a wave's fragment 0.
   constexpr int A2N = G::FUSED ? G::TAPS2 : 1;
   int aoff2[A2N][3], boff2[2], amask = 0;
-  const int ph = G::FUSED ? (wm * 96) / G::PHROWS : 0;
-  const bool has_m0 = G::FUSED && (wm * 96) % G::PHROWS == 0;
+  const int ph = G::W6 ? (wv >> 1) : G::FUSED ? (wm * 96) / G::PHROWS : 0;
+  const bool has_m0 = G::W6 || (G::FUSED && (wm * 96) % G::PHROWS == 0);
   if constexpr (G::FUSED) {
 #pragma unroll
     for (int k = 0; k < G::TAPS2; ++k) {
@@ -1276,6 +1309,26 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       const int n = wn * 64 + jn * 32 + lr;
       boff2[jn] = G::A2_BYTES + (ph * G::TAPS2 * NT + n) * ROWB + ((c0 ^ G::key(n)) << 4);
     }
+  }
+  // CONV_UP0_W6: wave = (phase w6e, column half w6h); A offsets per input position of the lane's sample
+  const int w6e = wv >> 1, w6h = wv & 1;
+  constexpr int W6P1 = G::W6 ? G::L : 1, W6P2 = G::W6 ? G::LH : 1;
+  int apos1[W6P1], apos2[W6P2];
+  if constexpr (G::W6) {
+    const int n = w6h * 32 + lr;
+    boff[0] = G::A_BYTES + n * ROWB + ((c0 ^ G::key(n)) << 4);
+    boff2[0] = G::A2_BYTES + (w6e * G::TAPS2 * NT + n) * ROWB + ((c0 ^ G::key(n)) << 4);
+#pragma unroll
+    for (int p = 0; p < G::L; ++p) {
+      const int row = G::slot1(p, lr);
+      apos1[p] = row * ROWB + ((c0 ^ G::key(row)) << 4);
+    }
+#pragma unroll
+    for (int q = 0; q < G::LH; ++q) {
+      const int row = q * G::S + lr;
+      apos2[q] = row * ROWB + ((c0 ^ G::key(row)) << 4);
+    }
+    amask = apos2[0];
   }
 
   f32x16 acc[3][2];
@@ -1344,7 +1397,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   if constexpr (G::FUSED) {
     const int n2 = P3 ? a.c2 / (G::KC / 2) : (XS ? 3 : 1) * (a.c2 / G::KC);
     ebase = reinterpret_cast<const char*>(a.epack) +
-            ((size_t)n_tile * n2 * 2 * NT + (size_t)ph * NT + wn * 64 + lr) * ROWB + h * 16;
+            ((size_t)n_tile * n2 * 2 * NT + (size_t)ph * NT + (G::W6 ? (wv & 1) * 32 : wn * 64) + lr) * ROWB + h * 16;
   }
   auto load_epk = [&](int kc2) {   // segment-2 chunk kc2's correction fragments
     if constexpr (G::FUSED) {
@@ -1352,7 +1405,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
 #pragma unroll
       for (int g = 0; g < NGE; ++g)
 #pragma unroll
-        for (int jn = 0; jn < 2; ++jn) epk[g][jn] = *reinterpret_cast<const fragT*>(p + jn * 32 * ROWB + g * 32);
+        for (int jn = 0; jn < (G::W6 ? 1 : 2); ++jn) epk[g][jn] = *reinterpret_cast<const fragT*>(p + jn * 32 * ROWB + g * 32);
     }
   };
   // NEXT = 2 (first chunk only): the pieces of chunks nkc and nkc + 1 (stages nbuf, nbuf + 1).
@@ -1363,7 +1416,95 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     constexpr int SEGV = (int)decltype(seg_tag)::value;
     constexpr int SEG = SEGV == 4 ? 2 : SEGV;
     char* nbase = smem + nbuf * G::STAGE;
-    if constexpr (G::ZS && CONV_UP0_ZS_CACHE) {
+    if constexpr (G::W6) {
+      // up0 zero-skip, 6 fragments per wave (CONV_UP0_W6): wave (phase PAT, column half); step st = (k-group
+      // g, tap zs_tap(jj)); reads: the step's B fragment, then the positions first needed at this tap in the
+      // first group of their A half; MFMAs of step st - 1: fragment f -> acc[f % 3][f / 3], A from zap.
+      constexpr int PAT = decltype(pat_tag)::value;
+      constexpr int NG = P3 ? 3 : ROWB / 32;
+      constexpr int NH = ROWB / 32;
+      constexpr int NT_ = SEG == 2 ? G::TAPS2 : TAPS;
+      constexpr int NS = NT_ * NG;
+      constexpr int NPER = NEXT == 3 ? G::PER2 : G::PER;
+      constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;
+      constexpr int PPS = (NPC + NS - 1) / NS;
+      static_assert(NS % 2 == 0 && (kg_a<P3>(NG - 1) >> 5) != 0, "B double buffer alternates per step; carried half");
+      fragT am[SEG == 2 ? NH : 1];
+      static_for<0, NS>([&](auto st_tag) {
+        constexpr int st = decltype(st_tag)::value;
+        constexpr int g = st / NT_, jj = st % NT_, sb = st & 1, pb = sb ^ 1;
+        constexpr int j = G::zs_tap(SEG, jj);
+        constexpr int ah = kg_a<P3>(g) >> 5;
+        constexpr bool fg = !P3 || g != 1;
+        constexpr int gp = st == 0 ? NG - 1 : (st - 1) / NT_;
+        constexpr int jpp = G::zs_tap(SEG, (st == 0 ? NS - 1 : st - 1) % NT_);
+        constexpr int ahp = kg_a<P3>(gp) >> 5;
+        const char* pb0 = base + (((SEG == 2 ? boff2[0] : boff[0]) + j * NT * ROWB) ^ kg_b<P3>(g));
+        auto body = [&](auto prev_tag) {
+          constexpr int PV = decltype(prev_tag)::value;   // 0: this segment's step st - 1; 1 / 2: segment 1's / 2's last
+          constexpr int SP = PV == 0 ? SEG : PV;
+          constexpr int TPP = PV == 0 ? jpp : SP == 2 ? G::TAPS2 - 1 : TAPS - 1;
+#define PETDIFF_WMF(f)                                                                                      \
+  if constexpr (G::w6_ok(SP, PAT, f, TPP) && !(CONV_EXP_MODE & 2))                                           \
+    acc[(f) % 3][(f) / 3] = mfma32(zap[ahp][G::w6_pos(SP, PAT, f, TPP)], bv[pb][0], acc[(f) % 3][(f) / 3]);
+#define PETDIFF_WRA(f)                                                                                      \
+  if constexpr (fg && G::w6_ok(SEG, PAT, f, j) && G::w6_first(SEG, PAT, f, jj) && !(CONV_EXP_MODE & 64)) {   \
+    constexpr int P_ = G::w6_pos(SEG, PAT, f, j);                                                            \
+    zap[ah][P_] = *reinterpret_cast<const fragT*>(base + ((SEG == 2 ? apos2[P_ < G::LH ? P_ : 0] : apos1[P_]) ^ kg_a<P3>(g))); \
+  }
+          PETDIFF_WMF(0)
+          if constexpr (!(CONV_EXP_MODE & 64)) bv[sb][0] = *reinterpret_cast<const fragT*>(pb0);
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_WMF(1)
+          PETDIFF_WRA(0)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_WMF(2)
+          PETDIFF_WRA(1)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_WMF(3)
+          PETDIFF_WRA(2)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_WMF(4)
+          PETDIFF_WRA(3)
+          __builtin_amdgcn_sched_barrier(0);
+          PETDIFF_WMF(5)
+          PETDIFF_WRA(4)
+          PETDIFF_WRA(5)
+#undef PETDIFF_WRA
+#undef PETDIFF_WMF
+        };
+        if constexpr (st > 0) body(std::integral_constant<int, 0>{});
+        else if constexpr (SEG == 1 || SEGV == 4) body(std::integral_constant<int, 1>{});
+        else body(std::integral_constant<int, 2>{});
+        if constexpr (SEG == 2) {
+          // left-edge correction of fragment 0 (m = 0), in the same place as the other paths
+          if (st == 0) {
+#pragma unroll
+            for (int gg = 0; gg < NH; ++gg) am[gg] = *reinterpret_cast<const fragT*>(base + (amask ^ (gg << 5)));
+          }
+          if (st == 1) {
+#pragma unroll
+            for (int gg = 0; gg < NG; ++gg)
+              if constexpr (!(CONV_EXP_MODE & 2)) acc[0][0] = mfma32(am[kg_a<P3>(gg) >> 5], epk[kg_b<P3>(gg) >> 5][0], acc[0][0]);
+            const int k2 = kc - dma.n1;
+            if (kc + 1 < NC) load_epk(k2 + 1);
+          }
+        }
+        if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
+#pragma unroll
+          for (int u = 0; u < PPS; ++u) {
+            const int k = st * PPS + u;
+            if (k < NPER) {
+              if constexpr (NEXT == 3) dma.piece2(nbase, k, nkc - dma.n1, lane);
+              else dma.piece1(nbase, k, nkc, lane);
+            } else if (NEXT == 2 && k < NPC) {
+              dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    } else if constexpr (G::ZS && CONV_UP0_ZS_CACHE) {
       // up0 zero-skip, A fragments cached per position (zap[half][position]): step st = (k-group g, tap
       // zs_tap(jj)); the reads of step st are B and the positions first needed at this tap in this half,
       // the MFMAs of step st - 1 take their A operand from zap.  zap[h] is rewritten only by a later chunk's
@@ -2170,16 +2311,25 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
             if (G::zs_valid2(PAT, i, G::TAPS2 - 1))
 #pragma unroll
               for (int jn = 0; jn < 2; ++jn)
-                if constexpr (!(CONV_EXP_MODE & 2)) {
+                if constexpr (!(CONV_EXP_MODE & 2) && !G::W6) {
                   if constexpr (CONV_UP0_ZS_CACHE)
                     acc[i][jn] = mfma32(zap[HL][G::zs_pos(2, PAT, i, G::TAPS2 - 1)], bv[1][jn], acc[i][jn]);
                   else
                     acc[i][jn] = mfma32(av[1][i], bv[1][jn], acc[i][jn]);
                 }
+          if constexpr (G::W6 && !(CONV_EXP_MODE & 2)) {
+#pragma unroll
+            for (int f = 0; f < 6; ++f)
+              if (G::w6_ok(2, PAT, f, G::TAPS2 - 1))
+                acc[f % 3][f / 3] = mfma32(zap[HL][G::w6_pos(2, PAT, f, G::TAPS2 - 1)], bv[1][0], acc[f % 3][f / 3]);
+          }
         }
       };
       // up0 zero-skip: each wave's fragment set gets its own main loop (no per-step branch)
-      if constexpr (G::ZS) {
+      if constexpr (G::W6) {
+        if (w6e == 0) fused_loop(P0{});
+        else fused_loop(std::integral_constant<int, 1>{});
+      } else if constexpr (G::ZS) {
         if (wmu == 0) fused_loop(P0{});
         else if (wmu == 1) fused_loop(std::integral_constant<int, 1>{});
         else if (wmu == 2) fused_loop(std::integral_constant<int, 2>{});
@@ -2427,8 +2577,9 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       for (int jn = 0; jn < 2; ++jn)
 #pragma unroll
         for (int rg = 0; rg < 16; rg += 2) {
-          const int r = G::frag_row(wmu, i) + (rg & 3) + 8 * (rg >> 2) + 4 * h;   // even
-          *reinterpret_cast<float2*>(ct + (r >> 1) * G::CT_LD + (wn * 64 + jn * 32 + lr) * 2) =
+          // W6: accumulator (i, jn) is fragment f = 3 jn + i (coarse row f of phase w6e), columns 32 w6h + lr
+          const int r = (G::W6 ? w6e * G::PHROWS + (3 * jn + i) * G::S : G::frag_row(wmu, i)) + (rg & 3) + 8 * (rg >> 2) + 4 * h;   // even
+          *reinterpret_cast<float2*>(ct + (r >> 1) * G::CT_LD + (G::W6 ? w6h * 32 + lr : wn * 64 + jn * 32 + lr) * 2) =
               make_float2(acc[i][jn][rg], acc[i][jn][rg + 1]);
         }
     __syncthreads();

@@ -1,5 +1,5 @@
 # Position-major down layers with cached A fragments (CONV_PM_CACHE=1, scripts/micro/alt/pc1.so) against the product:
-# bitwise, step layers in isolation, bench A/B (bf16, bf16x3).  Usage: bash scripts/gpu_zc_r3.sh TAG
+# bitwise, step layers in isolation, bench A/B (bf16, bf16x3).  Usage: bash scripts/gpu_pc_r3.sh TAG
 set -o pipefail
 TAG=${1:-zc}
 cd $GRAFT_REPO_ROOT
