@@ -140,6 +140,12 @@
 #ifndef CONV_PM_CACHE
 #define CONV_PM_CACHE 1
 #endif
+// Position-major down layers with 6 fragments per wave (as CONV_UP0_W6): wave w computes fragment set w >> 1
+// (down3: all 6 positions of sample half w >> 1; down2: positions {0,2,3,10,4,5} / {1,9,6,11,7,8}) for
+// output columns [32 (w & 1), +32): one B read per 6 MFMAs, the set's input positions read once per k-group.
+#ifndef CONV_PM_W6
+#define CONV_PM_W6 1
+#endif
 
 // Issue order of a step's 6 MFMAs (fragment i, B half jn): 0 = A-major (0,0) (0,1) (1,0) (1,1) (2,0)
 // (2,1), the reads interleaved a0 b0 b1 a1 a2; 1 = B-major (0,0) (1,0) (2,0) (0,1) (1,1) (2,1), consecutive
@@ -371,6 +377,23 @@ struct ConvGeom {
     for (int j2 = 0; j2 < j; ++j2)
       for (int i2 = 0; i2 < 3; ++i2)
         if (pm_valid(pat, i2, j2) && pm_pos(pat, i2) + j2 == pm_pos(pat, i) + j) return false;
+    return true;
+  }
+  // CONV_PM_W6: fragment f (0..5) of set `set` is position pw6_pos of sample half pw6_sh
+  static constexpr bool PW6 = PM && CONV_PM_CACHE && CONV_PM_W6;
+  static constexpr __device__ __host__ int pw6_pos(int set, int f) {
+    return L == 6 ? f
+                  : set == 0 ? (f == 0 ? 0 : f == 1 ? 2 : f == 2 ? 3 : f == 3 ? 10 : f == 4 ? 4 : 5)
+                             : (f == 0 ? 1 : f == 1 ? 9 : f == 2 ? 6 : f == 3 ? 11 : f == 4 ? 7 : 8);
+  }
+  static constexpr __device__ __host__ int pw6_sh(int set) { return L == 6 ? set : 0; }
+  static constexpr __device__ __host__ bool pw6_valid(int set, int f, int j) {
+    return pw6_pos(set, f) + j - PADL >= 0 && pw6_pos(set, f) + j - PADL < L;
+  }
+  static constexpr __device__ __host__ bool pw6_first(int set, int f, int j) {
+    for (int j2 = 0; j2 < j; ++j2)
+      for (int f2 = 0; f2 < 6; ++f2)
+        if (pw6_valid(set, f2, j2) && pw6_pos(set, f2) + j2 == pw6_pos(set, f) + j) return false;
     return true;
   }
   // position -> 3 pat + i (the inverse table)
@@ -1330,6 +1353,20 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     }
     amask = apos2[0];
   }
+  // CONV_PM_W6: wave = (fragment set pw6set, column half w6h); A offsets per input position
+  const int pw6set = wv >> 1;
+  constexpr int PW6P = G::PW6 ? G::L : 1;
+  int apm[PW6P];
+  if constexpr (G::PW6) {
+    const int n = w6h * 32 + lr;
+    boff[0] = G::A_BYTES + n * ROWB + ((c0 ^ G::key(n)) << 4);
+    const int sm = (pw6set & (G::L == 6 ? 1 : 0)) * 32 + lr;   // sample of this lane (down3: half pw6set)
+#pragma unroll
+    for (int p = 0; p < G::L; ++p) {
+      const int row = p * G::S + sm;
+      apm[p] = row * ROWB + ((c0 ^ G::key(row)) << 4);
+    }
+  }
 
   f32x16 acc[3][2];
 #pragma unroll
@@ -1849,6 +1886,63 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
 #pragma unroll
         for (int i = 0; i < 3; ++i) cav[i] = AP[NG - 1][jl + D * i];
       }
+    } else if constexpr (G::PW6) {
+      // position-major, 6 fragments per wave (CONV_PM_W6): step st = (tap j, k-group g) as the other PM
+      // paths; reads: the step's B fragment, then the set's positions first needed at tap j (first group of
+      // their half); MFMAs of step st - 1: fragment f -> acc[f % 3][f / 3], A from zap.
+      constexpr int NG = P3 ? 3 : ROWB / 32;
+      constexpr int NS = TAPS * NG;
+      constexpr int NPER = G::PER;
+      constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;
+      constexpr int PPS = (NPC + NS - 1) / NS;
+      constexpr int SET = decltype(pat_tag)::value;
+      static_assert(NS % 2 == 0 && (kg_a<P3>(NG - 1) >> 5) != 0, "B double buffer alternates per step; carried half");
+      static_for<0, NS>([&](auto st_tag) {
+        constexpr int st = decltype(st_tag)::value;
+        constexpr int j = st / NG, g = st % NG, sb = st & 1, pb = sb ^ 1;
+        constexpr int jp = st == 0 ? TAPS - 1 : (st - 1) / NG;
+        constexpr int gp = st == 0 ? NG - 1 : (st - 1) % NG;
+        constexpr int ah = kg_a<P3>(g) >> 5, ahp = kg_a<P3>(gp) >> 5;
+        constexpr bool fg = !P3 || g != 1;
+        const char* pb0 = base + ((boff[0] + j * NT * ROWB) ^ kg_b<P3>(g));
+#define PETDIFF_QMF(f)                                                                                      \
+  if constexpr (G::pw6_valid(SET, f, jp) && !(CONV_EXP_MODE & 2))                                           \
+    acc[(f) % 3][(f) / 3] = mfma32(zap[ahp][G::pw6_pos(SET, f) + jp - PADL], bv[pb][0], acc[(f) % 3][(f) / 3]);
+#define PETDIFF_QRA(f)                                                                                      \
+  if constexpr (fg && G::pw6_valid(SET, f, j) && G::pw6_first(SET, f, j) && !(CONV_EXP_MODE & 64)) {        \
+    constexpr int P_ = G::pw6_pos(SET, f) + j - PADL;                                                        \
+    zap[ah][P_] = *reinterpret_cast<const fragT*>(base + (apm[P_] ^ kg_a<P3>(g)));                           \
+  }
+        PETDIFF_QMF(0)
+        if constexpr (!(CONV_EXP_MODE & 64)) bv[sb][0] = *reinterpret_cast<const fragT*>(pb0);
+        __builtin_amdgcn_sched_barrier(0);
+        PETDIFF_QMF(1)
+        PETDIFF_QRA(0)
+        __builtin_amdgcn_sched_barrier(0);
+        PETDIFF_QMF(2)
+        PETDIFF_QRA(1)
+        __builtin_amdgcn_sched_barrier(0);
+        PETDIFF_QMF(3)
+        PETDIFF_QRA(2)
+        __builtin_amdgcn_sched_barrier(0);
+        PETDIFF_QMF(4)
+        PETDIFF_QRA(3)
+        __builtin_amdgcn_sched_barrier(0);
+        PETDIFF_QMF(5)
+        PETDIFF_QRA(4)
+        PETDIFF_QRA(5)
+#undef PETDIFF_QRA
+#undef PETDIFF_QMF
+        if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
+#pragma unroll
+          for (int u = 0; u < PPS; ++u) {
+            const int k = st * PPS + u;
+            if (k < NPER) dma.piece1(nbase, k, nkc, lane);
+            else if (NEXT == 2 && k < NPC) dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
     } else if constexpr (G::PM && CONV_PM_CACHE) {
       // position-major, A fragments cached per input position (zap[half][position], CONV_PM_CACHE): step
       // st = (tap j, k-group g); the reads of step st are B and the positions that this set first needs at
@@ -2430,7 +2524,15 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
           ring_barrier<0>();                               // B(kc+1): own LDS reads done
           buf = buf == 2 ? 0 : buf + 1;
         }
-        if constexpr (G::PM) {   // the last step (tap TAPS - 1) of this wave's valid fragments
+        if constexpr (G::PW6) {   // the last step (tap TAPS - 1) of this set's valid fragments
+          constexpr int SET = decltype(pat_tag)::value;
+          constexpr int HL = kg_a<P3>((P3 ? 3 : ROWB / 32) - 1) >> 5;
+#pragma unroll
+          for (int f = 0; f < 6; ++f)
+            if (G::pw6_valid(SET, f, TAPS - 1))
+              if constexpr (!(CONV_EXP_MODE & 2))
+                acc[f % 3][f / 3] = mfma32(zap[HL][G::pw6_pos(SET, f) + TAPS - 1 - PADL], bv[1][0], acc[f % 3][f / 3]);
+        } else if constexpr (G::PM) {   // the last step (tap TAPS - 1) of this wave's valid fragments
           constexpr int PAT = decltype(pat_tag)::value;
           constexpr int HL = kg_a<P3>((P3 ? 3 : ROWB / 32) - 1) >> 5;
 #pragma unroll
@@ -2447,7 +2549,10 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         }
       };
       // position-major: each fragment set gets its own main loop (no per-chunk branch)
-      if constexpr (G::PM && G::NPAT == 4) {
+      if constexpr (G::PW6) {
+        if (pw6set == 0) mainloop(P0{});
+        else mainloop(std::integral_constant<int, 1>{});
+      } else if constexpr (G::PM && G::NPAT == 4) {
         if (pm_pat == 0) mainloop(P0{});
         else if (pm_pat == 1) mainloop(std::integral_constant<int, 1>{});
         else if (pm_pat == 2) mainloop(std::integral_constant<int, 2>{});
@@ -2578,8 +2683,11 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
 #pragma unroll
         for (int rg = 0; rg < 16; rg += 2) {
           // W6: accumulator (i, jn) is fragment f = 3 jn + i (coarse row f of phase w6e), columns 32 w6h + lr
-          const int r = (G::W6 ? w6e * G::PHROWS + (3 * jn + i) * G::S : G::frag_row(wmu, i)) + (rg & 3) + 8 * (rg >> 2) + 4 * h;   // even
-          *reinterpret_cast<float2*>(ct + (r >> 1) * G::CT_LD + (G::W6 ? w6h * 32 + lr : wn * 64 + jn * 32 + lr) * 2) =
+          // PW6: fragment f = 3 jn + i is position pw6_pos(pw6set, f) of sample half pw6_sh, at its PM tile row
+          const int r = (G::W6    ? w6e * G::PHROWS + (3 * jn + i) * G::S
+                         : G::PW6 ? G::pm_row(G::pw6_pos(pw6set, 3 * jn + i), G::pw6_sh(pw6set) * 32)
+                                  : G::frag_row(wmu, i)) + (rg & 3) + 8 * (rg >> 2) + 4 * h;   // even
+          *reinterpret_cast<float2*>(ct + (r >> 1) * G::CT_LD + (G::W6 || G::PW6 ? w6h * 32 + lr : wn * 64 + jn * 32 + lr) * 2) =
               make_float2(acc[i][jn][rg], acc[i][jn][rg + 1]);
         }
     __syncthreads();
