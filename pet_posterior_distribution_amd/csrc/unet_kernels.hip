@@ -140,6 +140,13 @@
 #ifndef CONV_PM_CACHE
 #define CONV_PM_CACHE 1
 #endif
+// up1.fused (16 samples per tile: a fragment is two coarse rows m, m + 1 of 16 samples): the A fragment of
+// (fragment i, tap j) equals that of (i + 1, j - 4) in segment 1 and of (i + 1, k - 2) in segment 2, so each
+// k-group reads 14 of its 18 (segment 1) and 8 of its 12 (segment 2) A fragments, cached by key 4 i + j /
+// 2 i + k; a paired bf16x3 chunk's (a_hi, w_lo) group reuses the (a_hi, w_hi) group's.  0 = every read.
+#ifndef CONV_UP1_CACHE
+#define CONV_UP1_CACHE 1
+#endif
 // Position-major down layers with 6 fragments per wave (as CONV_UP0_W6): wave w computes fragment set w >> 1
 // (down3: all 6 positions of sample half w >> 1; down2: positions {0,2,3,10,4,5} / {1,9,6,11,7,8}) for
 // output columns [32 (w & 1), +32): one B read per 6 MFMAs, the set's input positions read once per k-group.
@@ -1413,6 +1420,13 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   constexpr bool ZAP = (G::ZS && CONV_UP0_ZS_CACHE) || (G::PM && CONV_PM_CACHE);
   constexpr int ZAP_H = ZAP ? 2 : 1, ZAP_P = ZAP ? G::L : 1;
   fragT zap[ZAP_H][ZAP_P];
+  // up1 A cache (CONV_UP1_CACHE): [32-B half][key 4 i + j (segment 1, 14 keys) / 2 i + k (segment 2, 8)]
+  constexpr bool UC = CONV_UP1_CACHE && G::FUSED && G::S == 16 && sizeof(T) == 2 && G::STAGES == 3;
+  fragT uca[UC ? 2 : 1][UC ? 14 : 1];
+#pragma unroll
+  for (int hh = 0; hh < (UC ? 2 : 1); ++hh)
+#pragma unroll
+    for (int p = 0; p < (UC ? 14 : 1); ++p) uca[hh][p] = fragT{};
 #pragma unroll
   for (int hh = 0; hh < ZAP_H; ++hh)
 #pragma unroll
@@ -2074,6 +2088,97 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+    } else if constexpr (UC) {
+      // up1 with cached A fragments (CONV_UP1_CACHE): step st = (tap j, k-group g) as the generic path;
+      // reads: B and the keys first needed at tap j (first group of their half); MFMAs of step st - 1 take
+      // A from uca[half][key].  At st = 0 they are the previous chunk's last step, of segment 1 for the
+      // first segment-2 chunk (SEGV == 4, peeled).
+      constexpr int NG = P3 ? 3 : ROWB / 32;
+      constexpr int NH = ROWB / 32;
+      constexpr int NT_ = SEG == 2 ? G::TAPS2 : TAPS;
+      constexpr int NS = NT_ * NG;
+      constexpr int NPER = NEXT == 3 ? G::PER2 : G::PER;
+      constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;
+      constexpr int PPS = (NPC + NS - 1) / NS;
+      constexpr int KS = SEG == 2 ? 2 : 4;                // key step between fragments
+      static_assert(NS % 2 == 0 && (kg_a<P3>(NG - 1) >> 5) != 0, "B double buffer alternates per step; carried half");
+      fragT am[SEG == 2 ? NH : 1];
+      static_for<0, NS>([&](auto st_tag) {
+        constexpr int st = decltype(st_tag)::value;
+        constexpr int j = st / NG, g = st % NG, sb = st & 1, pb = sb ^ 1;
+        constexpr int gp = st == 0 ? NG - 1 : (st - 1) % NG;
+        constexpr int ah = kg_a<P3>(g) >> 5, ahp = kg_a<P3>(gp) >> 5;
+        constexpr bool fg = !P3 || g != 1;
+        // previous step's segment key step and tap
+        constexpr int KSP = st > 0 ? KS : (SEG == 1 || SEGV == 4) ? 4 : 2;
+        constexpr int JP = st > 0 ? (st - 1) / NG : (SEG == 1 || SEGV == 4) ? TAPS - 1 : G::TAPS2 - 1;
+        int ao0, ao1, ao2, bo0, bo1;
+        if constexpr (SEG == 2) {
+          ao0 = aoff2[j][0]; ao1 = aoff2[j][1]; ao2 = aoff2[j][2]; bo0 = boff2[0]; bo1 = boff2[1];
+        } else {
+          ao0 = aoff[j][0]; ao1 = aoff[j][1]; ao2 = aoff[j][2]; bo0 = boff[0]; bo1 = boff[1];
+        }
+        const char* pa0 = base + (ao0 ^ kg_a<P3>(g));
+        const char* pa1 = base + (ao1 ^ kg_a<P3>(g));
+        const char* pa2 = base + (ao2 ^ kg_a<P3>(g));
+        const char* pb0 = base + ((bo0 + j * NT * ROWB) ^ kg_b<P3>(g));
+        const char* pb1 = base + ((bo1 + j * NT * ROWB) ^ kg_b<P3>(g));
+        // (i, j) is the first reader of key KS i + j unless (i + 1, j - KS) read it (j >= KS, i <= 1)
+#define PETDIFF_UMF(i, jn) \
+  if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(uca[ahp][KSP * (i) + JP], bv[pb][jn], acc[i][jn]);
+#define PETDIFF_URA(i, ptr)                                                                                 \
+  if constexpr (fg && !(j >= KS && (i) <= 1) && !(CONV_EXP_MODE & 64))                                       \
+    uca[ah][KS * (i) + j] = *reinterpret_cast<const fragT*>(ptr);
+#define PETDIFF_URB(dst, ptr) \
+  if constexpr (!(CONV_EXP_MODE & 64)) dst = *reinterpret_cast<const fragT*>(ptr);
+        PETDIFF_UMF(0, 0)
+        PETDIFF_URA(0, pa0)
+        __builtin_amdgcn_sched_barrier(0);
+        PETDIFF_UMF(1, 0)
+        PETDIFF_URB(bv[sb][0], pb0)
+        __builtin_amdgcn_sched_barrier(0);
+        PETDIFF_UMF(2, 0)
+        PETDIFF_URA(1, pa1)
+        __builtin_amdgcn_sched_barrier(0);
+        PETDIFF_UMF(0, 1)
+        PETDIFF_URA(2, pa2)
+        __builtin_amdgcn_sched_barrier(0);
+        PETDIFF_UMF(1, 1)
+        PETDIFF_URB(bv[sb][1], pb1)
+        __builtin_amdgcn_sched_barrier(0);
+        PETDIFF_UMF(2, 1)
+#undef PETDIFF_URB
+#undef PETDIFF_URA
+#undef PETDIFF_UMF
+        if constexpr (SEG == 2) {
+          if (st == 0 && has_m0) {
+#pragma unroll
+            for (int gg = 0; gg < NH; ++gg) am[gg] = *reinterpret_cast<const fragT*>(base + (amask ^ (gg << 5)));
+          }
+          if (st == 1 && has_m0) {
+#pragma unroll
+            for (int gg = 0; gg < NG; ++gg)
+#pragma unroll
+              for (int jn = 0; jn < 2; ++jn)
+                if constexpr (!(CONV_EXP_MODE & 2)) acc[0][jn] = mfma32(am[kg_a<P3>(gg) >> 5], epk[kg_b<P3>(gg) >> 5][jn], acc[0][jn]);
+            const int k2 = kc - dma.n1;
+            if (kc + 1 < NC) load_epk(k2 + 1);
+          }
+        }
+        if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
+#pragma unroll
+          for (int u = 0; u < PPS; ++u) {
+            const int k = st * PPS + u;
+            if (k < NPER) {
+              if constexpr (NEXT == 3) dma.piece2(nbase, k, nkc - dma.n1, lane);
+              else dma.piece1(nbase, k, nkc, lane);
+            } else if (NEXT == 2 && k < NPC) {
+              dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
     } else if constexpr (sizeof(T) == 2) {
       constexpr int NG = P3 ? 3 : ROWB / 32;   // k-groups per chunk (paired bf16x3: 3)
       constexpr int NH = ROWB / 32;             // 32-B halves of a row
@@ -2381,7 +2486,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
           ring_barrier<G::PER2>();
           buf = buf == 2 ? 0 : buf + 1;
         }
-        if constexpr (G::ZS) {   // the first segment-2 chunk, peeled (n2 >= 3: up0 has 32, bf16x3 96)
+        if constexpr (G::ZS || UC) {   // the first segment-2 chunk, peeled (n2 >= 3: up0 32 / 96, up1 16 / 32)
           compute(smem + buf * G::STAGE, Seg2Next{}, kc + 2, buf == 0 ? 2 : buf - 1, Seg2First{}, kc, pat_tag);
           ring_barrier<G::PER2>();
           buf = buf == 2 ? 0 : buf + 1;
@@ -2625,6 +2730,13 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(cav[i], bv[1][jn], acc[i][jn]);
   } else if constexpr (G::PM || G::ZS) {
     // flushed at the end of the position-major / zero-skip main loop
+  } else if constexpr (UC) {   // the last chunk's last step: composite tap 3 of the last group's half
+    constexpr int HL = kg_a<P3>((P3 ? 3 : ROWB / 32) - 1) >> 5;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn)
+        if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(uca[HL][2 * i + G::TAPS2 - 1], bv[1][jn], acc[i][jn]);
   } else {
     mfma_bf16(1);   // the last chunk's last step (NS even)
   }
