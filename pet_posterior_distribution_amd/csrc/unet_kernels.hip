@@ -147,6 +147,12 @@
 #ifndef CONV_UP1_CACHE
 #define CONV_UP1_CACHE 1
 #endif
+// down1 with the pair-position-major layout (CONV_DOWN1_PP) and the same keyed cache: fragment F holds
+// positions 2F, 2F + 1 of the tile's 16 samples, so (F, j) reads what (F + 1, j - 2) read (key 2 F + j):
+// 10 of a k-group's 18 A fragments.  Needs CONV_DOWN1_PP=1.
+#ifndef CONV_DOWN1_CACHE
+#define CONV_DOWN1_CACHE 0
+#endif
 // Position-major down layers with 6 fragments per wave (as CONV_UP0_W6): wave w computes fragment set w >> 1
 // (down3: all 6 positions of sample half w >> 1; down2: positions {0,2,3,10,4,5} / {1,9,6,11,7,8}) for
 // output columns [32 (w & 1), +32): one B read per 6 MFMAs, the set's input positions read once per k-group.
@@ -1421,7 +1427,8 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   constexpr int ZAP_H = ZAP ? 2 : 1, ZAP_P = ZAP ? G::L : 1;
   fragT zap[ZAP_H][ZAP_P];
   // up1 A cache (CONV_UP1_CACHE): [32-B half][key 4 i + j (segment 1, 14 keys) / 2 i + k (segment 2, 8)]
-  constexpr bool UC = CONV_UP1_CACHE && G::FUSED && G::S == 16 && sizeof(T) == 2 && G::STAGES == 3;
+  constexpr bool UC = (CONV_UP1_CACHE && G::FUSED && G::S == 16 && sizeof(T) == 2 && G::STAGES == 3) ||
+                     (CONV_DOWN1_CACHE && G::PP);
   fragT uca[UC ? 2 : 1][UC ? 14 : 1];
 #pragma unroll
   for (int hh = 0; hh < (UC ? 2 : 1); ++hh)
@@ -2100,7 +2107,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       constexpr int NPER = NEXT == 3 ? G::PER2 : G::PER;
       constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;
       constexpr int PPS = (NPC + NS - 1) / NS;
-      constexpr int KS = SEG == 2 ? 2 : 4;                // key step between fragments
+      constexpr int KS = (SEG == 2 || G::PP) ? 2 : 4;     // key step between fragments
       static_assert(NS % 2 == 0 && (kg_a<P3>(NG - 1) >> 5) != 0, "B double buffer alternates per step; carried half");
       fragT am[SEG == 2 ? NH : 1];
       static_for<0, NS>([&](auto st_tag) {
@@ -2110,7 +2117,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         constexpr int ah = kg_a<P3>(g) >> 5, ahp = kg_a<P3>(gp) >> 5;
         constexpr bool fg = !P3 || g != 1;
         // previous step's segment key step and tap
-        constexpr int KSP = st > 0 ? KS : (SEG == 1 || SEGV == 4) ? 4 : 2;
+        constexpr int KSP = st > 0 ? KS : G::PP ? 2 : (SEG == 1 || SEGV == 4) ? 4 : 2;
         constexpr int JP = st > 0 ? (st - 1) / NG : (SEG == 1 || SEGV == 4) ? TAPS - 1 : G::TAPS2 - 1;
         int ao0, ao1, ao2, bo0, bo1;
         if constexpr (SEG == 2) {
@@ -2736,7 +2743,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int jn = 0; jn < 2; ++jn)
-        if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(uca[HL][2 * i + G::TAPS2 - 1], bv[1][jn], acc[i][jn]);
+        if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(uca[HL][2 * i + (G::PP ? TAPS : G::TAPS2) - 1], bv[1][jn], acc[i][jn]);
   } else {
     mfma_bf16(1);   // the last chunk's last step (NS even)
   }

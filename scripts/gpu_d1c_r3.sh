@@ -1,0 +1,17 @@
+# down1 pair-position-major + keyed A cache (scripts/micro/alt/d1c.so) and pair-position-major alone
+# (d1pp.so) against the product: bitwise, bench A/B (bf16, bf16x3).  Usage: bash scripts/gpu_d1c_r3.sh TAG
+set -o pipefail
+TAG=${1:-d1c}
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+( export PETDIFF_LIB=$GRAFT_REPO_ROOT/scripts/micro/alt/d1c.so; timeout -k 10 300 python scripts/lib_bitwise.py dump $OUT/d1c.npz ) > $OUT/bitwise.txt 2>&1 || exit 1
+timeout -k 10 300 python scripts/lib_bitwise.py dump $OUT/cur.npz >> $OUT/bitwise.txt 2>&1 || exit 1
+python scripts/lib_bitwise.py compare $OUT/cur.npz $OUT/d1c.npz >> $OUT/bitwise.txt 2>&1
+tail -1 $OUT/bitwise.txt
+rm -f $OUT/*.npz
+ALT=d1c.so REPS=3 bash scripts/ab_bench.sh $TAG/ab || exit 1
+ALT=d1pp.so REPS=2 bash scripts/ab_bench.sh $TAG/ab_pp || exit 1
+ALT=d1c.so REPS=2 ARGS="--steps 2 --dtype bf16x3" bash scripts/ab_bench.sh $TAG/ab_x3 || exit 1
+echo EXIT 0
