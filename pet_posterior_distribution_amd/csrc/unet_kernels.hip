@@ -153,6 +153,15 @@
 #ifndef CONV_DOWN1_CACHE
 #define CONV_DOWN1_CACHE 0
 #endif
+// Final level: its 49 KB of time / label map rows go out after segment-1 chunk FIN_MAPS_KM's pieces, in the
+// middle of the K loop, instead of beside chunk 0 in the start-up burst of all 256 workgroups; the ring
+// barriers after chunks KM and KM + 1 allow them in flight (counted vmcnt), the one after KM + 2 retires them.
+#ifndef CONV_FIN_MAPS_MID
+#define CONV_FIN_MAPS_MID 0
+#endif
+#ifndef FIN_MAPS_KM
+#define FIN_MAPS_KM 2
+#endif
 // Position-major down layers with 6 fragments per wave (as CONV_UP0_W6): wave w computes fragment set w >> 1
 // (down3: all 6 positions of sample half w >> 1; down2: positions {0,2,3,10,4,5} / {1,9,6,11,7,8}) for
 // output columns [32 (w & 1), +32): one B read per 6 MFMAs, the set's input positions read once per k-group.
@@ -2459,9 +2468,10 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       // kernel start all 256 workgroups' bursts share the fabric, so the final level's 50 KB of map
       // rows per workgroup would delay every chunk 0 (prologue 4.6 us on up2 against 2.8 on up0);
       // issued after B0 they stream during the K loop and still retire at B1.
+      constexpr bool FINMID = CONV_FIN_MAPS_MID && G::FIN_MAPS && !CONV_MAPS_LATE;
       if constexpr (!CONV_MAPS_LATE) {
         prefetch_maps();
-        prefetch_fin_maps();
+        if constexpr (!FINMID) prefetch_fin_maps();
       }
       // B0: chunk 0 landed; the maps (issued after it, NMAPW per wave) may still be in flight --
       // B1 below retires them together with chunk 1, long before the epilogue reads them
@@ -2470,6 +2480,8 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         ring_barrier<0>();
         prefetch_maps();
         prefetch_fin_maps();
+      } else if constexpr (FINMID) {
+        ring_barrier<NMAPW - G::FMAP_FULL>();          // the final maps go out later (FIN_MAPS_KM)
       } else if (map_extra) {
         ring_barrier<NMAPW + 1>();
       } else {
@@ -2485,7 +2497,19 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         int buf = 1, kc = 1;
         for (; kc + 2 < n1; ++kc) {
           compute(smem + buf * G::STAGE, Yes{}, kc + 2, buf == 0 ? 2 : buf - 1, Seg1{}, 0, pat_tag);
-          ring_barrier<G::PER>();
+          if constexpr (FINMID) {
+            static_assert(!FINMID || FIN_MAPS_KM >= 1, "maps after the first loop chunk");
+            // host guarantees n1 >= FIN_MAPS_KM + 4 on the final level (n1 = 8 bf16 / fp16, 24 bf16x3)
+            if (kc == FIN_MAPS_KM) prefetch_fin_maps();
+            if (kc == FIN_MAPS_KM || kc == FIN_MAPS_KM + 1) {
+              if (map_extra) ring_barrier<G::PER + G::FMAP_FULL + 1>();
+              else ring_barrier<G::PER + G::FMAP_FULL>();
+            } else {
+              ring_barrier<G::PER>();
+            }
+          } else {
+            ring_barrier<G::PER>();
+          }
           buf = buf == 2 ? 0 : buf + 1;
         }
         for (; kc < n1; ++kc) {                              // the next chunks are segment 2
