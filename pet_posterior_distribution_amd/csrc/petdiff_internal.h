@@ -160,7 +160,14 @@ constexpr int layer_ntile(int kind) { return 64 * layer_tile(kind).wn; }
 #ifndef CONV_X3_PAIRED
 #define CONV_X3_PAIRED 1
 #endif
-constexpr bool x3_paired(int kind) { return CONV_X3_PAIRED && layer_tile(kind).rowb == 64 && kind != LK_DOWN1; }
+// down2 / down3 separately (their loader waves hide most of the stream; A/B switch)
+#ifndef CONV_X3_PAIRED_PM
+#define CONV_X3_PAIRED_PM 1
+#endif
+constexpr bool x3_paired(int kind) {
+  return CONV_X3_PAIRED && layer_tile(kind).rowb == 64 && kind != LK_DOWN1 &&
+         (CONV_X3_PAIRED_PM || (kind != LK_DOWN2 && kind != LK_DOWN3));
+}
 template <typename T>
 constexpr int layer_kc(int kind) { return layer_tile(kind).rowb / (int)sizeof(T); }
 
