@@ -203,7 +203,9 @@ def load_pmc(fused_up=False, dtype='bfloat16'):
         out = {k: d.get(pre + suf) for k, suf in (('traffic', '_bytes_per_launch'), ('mfma_busy', '_mfma_busy_cycles'),
                                                   ('grbm', '_grbm_gui_active'), ('source', '_source'))}
     out['code_hash'] = now
-    out['stale'] = have != now
+    # no hash for this build (e.g. a code-object bundle the parser does not recognise): the counters
+    # cannot be matched to it, so they are stale, not a match of two Nones
+    out['stale'] = now is None or have != now
     out['counted_on'] = have
     return out
 

@@ -114,7 +114,6 @@ struct DevBuf {
   template <typename T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 
-constexpr int kMaxSplit = 2;   // sample ranges of a split generate (PETDIFF_SPLIT)
 
 struct GraphEntry {
   hipGraphExec_t exec = nullptr;
@@ -152,19 +151,8 @@ struct petdiff_ctx {
   // run the next step's down0 inside the previous step's up2.block epilogue (generate);
   // PETDIFF_FUSE_DOWN0=0 restores the standalone down0 launch per step (A/B switch)
   bool fuse_down0 = true;
-  // ... and the next step's down1 too (16-bit networks; PETDIFF_FUSE_DOWN1=1).  Bitwise equal; measured a
-  // wash against the standalone launch in round 3 (bf16 -0.1..-0.6 %, bf16x3 0..+0.6 %, fp16 -0.5..+0.1 %,
-  // in-process A/B, profiles/r03/fused_down1), so off by default
-  bool fuse_down1 = false;
-  // down2 -> down3 in one launch with per-sample-block hand-off counters (PETDIFF_SEAM23=1, 16-bit
-  // networks; an experiment); seam: its counters (zeroed once, reset by each launch)
-  bool seam23 = false;
-  DevBuf seam;
   DevBuf xa, xb, tacbuf, tbuf, rng;
   hipStream_t cap_stream = nullptr;
-  hipStream_t split_stream = nullptr;  // second launch stream of a split generate (PETDIFF_SPLIT)
-  hipEvent_t split_ev[2] = {nullptr, nullptr};
-  int split = 1;
   int seg_steps = 0;                   // reverse steps per captured graph segment (0: the whole loop)
   std::map<std::vector<int>, GraphEntry> graphs;
   // timing
@@ -395,9 +383,7 @@ int ensure_workspace(petdiff_ctx* h, int B) {
   HIPC(h->xb.alloc(Bz * 96 * 4));
   HIPC(h->tacbuf.alloc(Bz * 4));
   HIPC(h->tbuf.alloc(Bz * 4));
-  HIPC(h->rng.alloc(16 * kMaxSplit));
-  HIPC(h->seam.alloc(((size_t)(B + 63) / 64 + 2) * 4));
-  HIPC(hipMemset(h->seam.p, 0, ((size_t)(B + 63) / 64 + 2) * 4));
+  HIPC(h->rng.alloc(16));
   // workspace moved: cached graphs hold stale pointers
   for (auto& kv : h->graphs) {
     if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
@@ -426,10 +412,8 @@ struct StepIO {
   FinalArgs fin;
   int s0_sel;                 // skip buffer of this step: 0 -> s0, 1 -> s0b
   bool skip_down0;            // s0/p0 already written by the previous step's fused epilogue
-  bool d1_ok;                 // generate: the fused epilogue may also run the next step's down1
   bool fuse_next;             // up2.block epilogue also runs down0 of the next step (t = next_t)
   int next_t;
-  int b_off;                  // first sample of this launch inside the workspace (split streams)
 };
 
 template <typename T>
@@ -450,24 +434,19 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
     }
     return PETDIFF_OK;
   };
-  // workspace buffers are sample-major: a launch over samples [b_off, b_off + B) uses slices
-  const size_t e = h->act_bytes(), bo = (size_t)io.b_off;
-  auto ws = [&](const DevBuf& d, size_t per_sample) -> void* {
-    return static_cast<char*>(d.p) + bo * per_sample * e;
-  };
-  void* s0 = io.s0_sel ? ws(h->s0b, 48 * 128) : ws(h->s0, 48 * 128);
-  void* s0_other = io.s0_sel ? ws(h->s0, 48 * 128) : ws(h->s0b, 48 * 128);
-  void* p0 = ws(h->p0, 24 * 128);
-  void* s1 = ws(h->s1, 24 * 256);
-  void* p1 = ws(h->p1, 12 * 256);
-  void* s2 = ws(h->s2, 12 * 512);
-  void* p2 = ws(h->p2, 6 * 512);
-  void* d3 = ws(h->d3, 6 * 1024);
-  void* u0 = ws(h->u0, 12 * 512);
-  void* b0 = ws(h->b0, 12 * 512);
-  void* u1 = ws(h->u1, 24 * 256);
-  void* b1 = ws(h->b1, 24 * 256);
-  void* u2 = ws(h->u2, 48 * 128);
+  void* s0 = io.s0_sel ? h->s0b.p : h->s0.p;
+  void* s0_other = io.s0_sel ? h->s0.p : h->s0b.p;
+  void* p0 = h->p0.p;
+  void* s1 = h->s1.p;
+  void* p1 = h->p1.p;
+  void* s2 = h->s2.p;
+  void* p2 = h->p2.p;
+  void* d3 = h->d3.p;
+  void* u0 = h->u0.p;
+  void* b0 = h->b0.p;
+  void* u1 = h->u1.p;
+  void* b1 = h->b1.p;
+  void* u2 = h->u2.p;
   Down0Args d0{};
   d0.x = io.x_in;
   d0.w0 = h->w0.as<float>();
@@ -480,10 +459,6 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
   d0.p0 = p0;
   d0.B = B;
   if (!io.skip_down0) CHK(timed(0, [&] { return launch_down0<T>(d0, s, h->x3); }));
-  // fused down1 (16-bit networks: bf16, fp16, bf16x3; any conditions): the previous step's epilogue wrote
-  // s1 / p1.  The kernel runs it on every tile whenever d1_w is set (tiles with several conditions read
-  // per-sample maps), so the host's decision to skip the launch is the only one
-  const bool d1_fuse = io.d1_ok && sizeof(T) == 2 && h->fuse_up;
 
   struct LIO { const void* s1; int c1; const void* s2; int c2; void* out; void* pool; };
   const LIO lio[kNumConvLayers] = {
@@ -532,45 +507,9 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
           a.fin.next.tvec = nullptr;
           a.fin.next.t_uniform = io.next_t;
           a.fin.next.s0 = s0_other;
-          if (d1_fuse) {   // s1 / p1 are dead once up1 and down2 of this step have run
-            const int lv = kConv[LK_DOWN1].cond_level;
-            a.fin.d1_w = h->wpack[LK_DOWN1].p;
-            a.fin.d1_tmap = h->tmap[lv].as<float>();
-            a.fin.d1_cmap = h->cmap[lv].as<float>();
-            a.fin.d1_s1 = s1;
-            a.fin.d1_p1 = p1;
-          }
         }
       }
       CHK(timed(1 + li, [&] { return launch_conv<T>(fl.kind, a, s, h->x3); }));
-      continue;
-    }
-    if (li == LK_DOWN1 && d1_fuse && io.skip_down0) continue;   // done by the previous step's epilogue
-    auto conv_args = [&](int lj) {
-      const ConvLayer& c = kConv[lj];
-      ConvArgs<T> x{};
-      x.src1 = reinterpret_cast<const T*>(lio[lj].s1);
-      x.c1 = lio[lj].c1;
-      x.src2 = reinterpret_cast<const T*>(lio[lj].s2);
-      x.c2 = lio[lj].c2;
-      x.wpack = h->wpack[lj].as<T>();
-      x.out = reinterpret_cast<T*>(lio[lj].out);
-      x.out_pool = reinterpret_cast<T*>(lio[lj].pool);
-      x.cmap = h->cmap[c.cond_level].as<float>();
-      x.tmap = h->tmap[c.cond_level].as<float>();
-      x.tac = io.tac;
-      x.tvec = io.tvec;
-      x.t_uniform = io.t_uniform;
-      x.n_t = h->T;
-      x.n_tac = h->n_tac;
-      x.B = B;
-      x.cout = c.cout;
-      return x;
-    };
-    if (li == LK_DOWN2 && h->seam23 && sizeof(T) == 2) {     // down2 + down3 in one launch
-      const ConvArgs<T> a2 = conv_args(LK_DOWN2), a3 = conv_args(LK_DOWN3);
-      CHK(timed(1 + li, [&] { return launch_seam23<T>(a2, a3, h->seam.as<int>(), s, h->x3); }));
-      ++li;                                                      // down3 ran in the same launch
       continue;
     }
     ConvArgs<T> a{};
@@ -709,8 +648,6 @@ int petdiff_create(const petdiff_config* cfg, const float* weights, size_t n_wei
   h->x3 = cfg->dtype == PETDIFF_DTYPE_BF16X3;
   h->spec = make_spec(*cfg, h->n_out);
   if (const char* e = std::getenv("PETDIFF_FUSE_DOWN0")) h->fuse_down0 = std::atoi(e) != 0;
-  if (const char* e = std::getenv("PETDIFF_FUSE_DOWN1")) h->fuse_down1 = std::atoi(e) != 0;
-  if (const char* e = std::getenv("PETDIFF_SEAM23")) h->seam23 = std::atoi(e) != 0 && cfg->dtype != PETDIFF_DTYPE_F32;
   h->fuse_up = cfg->dtype != PETDIFF_DTYPE_F32;
   if (const char* e = std::getenv("PETDIFF_FUSE_UP")) h->fuse_up = h->fuse_up && std::atoi(e) != 0;
   const size_t need = h->spec.back().off + h->spec.back().size;
@@ -720,13 +657,7 @@ int petdiff_create(const petdiff_config* cfg, const float* weights, size_t n_wei
   for (auto& s : h->spec) h->off[s.name] = s.off;
   HIPC(hipSetDevice(device));
   HIPC(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
-  if (const char* e = std::getenv("PETDIFF_SPLIT")) h->split = std::max(1, std::min(kMaxSplit, std::atoi(e)));
   if (const char* e = std::getenv("PETDIFF_GRAPH_SEG")) h->seg_steps = std::max(0, std::atoi(e));
-  if (h->split > 1) {
-    HIPC(hipStreamCreateWithFlags(&h->split_stream, hipStreamNonBlocking));
-    HIPC(hipEventCreateWithFlags(&h->split_ev[0], hipEventDisableTiming));
-    HIPC(hipEventCreateWithFlags(&h->split_ev[1], hipEventDisableTiming));
-  }
   HIPC(h->w32.alloc(need * 4));
   HIPC(hipMemcpy(h->w32.p, weights, need * 4, hipMemcpyHostToDevice));
   std::vector<float> host(weights, weights + need);
@@ -778,9 +709,6 @@ int petdiff_destroy(petdiff_handle h) {
   }
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
-  if (h->split_stream) (void)hipStreamDestroy(h->split_stream);
-  for (auto& ev : h->split_ev)
-    if (ev) (void)hipEventDestroy(ev);
   delete h;
   return PETDIFF_OK;
 }
@@ -880,7 +808,7 @@ int petdiff_p_sample(petdiff_handle h, const float* x, const int32_t* t, const i
   if (B == 0) return PETDIFF_OK;
   CHK(ensure_workspace(h, B));
   hipStream_t s = (hipStream_t)stream;
-  HIPC(launch_set_rng(h->rng.as<unsigned long long>(), seed, sample_offset, 0, 1, s));
+  HIPC(launch_set_rng(h->rng.as<unsigned long long>(), seed, sample_offset, s));
   StepIO io{};
   io.x_in = x;
   io.t_uniform = -1;
@@ -908,20 +836,13 @@ int petdiff_generate(petdiff_handle h, const float* x_T, const int32_t* tac, con
   for (int i = 0; i < n_steps; ++i)
     if (t_seq[i] < 0 || t_seq[i] >= h->T) return fail(PETDIFF_ERR_INVALID, "timestep index out of range");
   CHK(ensure_workspace(h, B));
-  // the loop overwrites the level buffers (with the fused down0 / down1, s0 / s1 / p1 end up holding the
-  // next step's data): petdiff_get_activation fails until a forward / p_sample runs again
+  // the loop overwrites the level buffers (with the fused down0, s0 / p0 end up holding the next step's
+  // data): petdiff_get_activation fails until a forward / p_sample runs again
   h->last_B = 0;
   hipStream_t s = (hipStream_t)stream;
   const size_t xbytes = (size_t)B * h->cfg.n_roi * h->cfg.n_par * 4;
   const bool graph = use_graph && !z_all && !all_xt && !h->timing && n_steps > 0;
-  // PETDIFF_SPLIT=2: the batch runs as two independent sample ranges, each its own graph,
-  // on two streams, so one range's launch boundaries overlap the other's main loops.
-  const int parts = (graph && h->split > 1 && B >= 64) ? h->split : 1;
-  int pb[kMaxSplit + 1];
-  for (int k = 0; k <= parts; ++k) pb[k] = k == parts ? B : (int)((long long)B * k / parts / 32 * 32);
-  static_assert(kMaxSplit == 2, "set_rng_kernel writes at most two pairs");
-  HIPC(launch_set_rng(h->rng.as<unsigned long long>(), seed, sample_offset,
-                      sample_offset + (unsigned long long)pb[parts > 1 ? 1 : 0], parts, s));
+  HIPC(launch_set_rng(h->rng.as<unsigned long long>(), seed, sample_offset, s));
   HIPC(hipMemcpyAsync(h->xa.p, x_T, xbytes, hipMemcpyDeviceToDevice, s));
   const int* tacp = nullptr;
   if (tac) {
@@ -929,36 +850,32 @@ int petdiff_generate(petdiff_handle h, const float* x_T, const int32_t* tac, con
     tacp = h->tacbuf.as<int>();
   }
   float* bufs[2] = {h->xa.as<float>(), h->xb.as<float>()};
-  auto enqueue = [&](hipStream_t q, int k, int i0, int i1) -> int {
-    const int b0 = pb[k], Bk = pb[k + 1] - pb[k];
+  auto enqueue = [&](hipStream_t q, int i0, int i1) -> int {
     for (int i = i0; i < i1; ++i) {
       StepIO io{};
-      io.x_in = bufs[i & 1] + (size_t)b0 * 96;
+      io.x_in = bufs[i & 1];
       io.t_uniform = t_seq[i];
       io.tvec = nullptr;
-      io.tac = tacp ? tacp + b0 : nullptr;
-      io.b_off = b0;
+      io.tac = tacp;
       io.fin = base_final(h);
-      io.fin.rng = h->rng.as<unsigned long long>() + 2 * k;
       io.fin.x_t = io.x_in;
       io.fin.z = z_all ? z_all + (size_t)i * B * 96 : nullptr;
       io.fin.rng_step = i;
       io.fin.flag_var_tilde = flag_var_tilde;
-      io.fin.x_next = bufs[(i + 1) & 1] + (size_t)b0 * 96;
+      io.fin.x_next = bufs[(i + 1) & 1];
       io.fin.x_all = all_xt ? all_xt + (size_t)i * B * 96 : nullptr;
       if (h->fuse_down0) {
         io.s0_sel = i & 1;
         io.skip_down0 = i > 0;
         io.fuse_next = i + 1 < n_steps;
         io.next_t = io.fuse_next ? t_seq[i + 1] : -1;
-        io.d1_ok = h->fuse_down1;
       }
-      CHK(network(h, io, Bk, q));
+      CHK(network(h, io, B, q));
     }
     return PETDIFF_OK;
   };
   if (!graph) {
-    CHK(enqueue(s, 0, 0, n_steps));
+    CHK(enqueue(s, 0, n_steps));
   } else {
     // The loop is captured as graph segments of seg_steps reverse steps (default: the whole loop in one):
     // hipGraphLaunch enqueues a graph's kernel nodes on the host, so a 5000-node graph costs milliseconds
@@ -966,42 +883,30 @@ int petdiff_generate(petdiff_handle h, const float* x_T, const int32_t* tac, con
     // the others are enqueued while the GPU runs the earlier ones.
     const int seg = h->seg_steps > 0 ? std::min(h->seg_steps, n_steps) : n_steps;
     const int nseg = (n_steps + seg - 1) / seg;
-    std::vector<hipGraphExec_t> ex((size_t)parts * nseg);
-    for (int k = 0; k < parts; ++k)
-      for (int sg = 0; sg < nseg; ++sg) {
-        const int i0 = sg * seg, i1 = std::min(n_steps, i0 + seg);
-        std::vector<int> key{B, flag_var_tilde, tac ? 1 : 0, n_steps, parts, k, i0, i1};
-        key.insert(key.end(), t_seq, t_seq + n_steps);
-        auto it = h->graphs.find(key);
-        if (it == h->graphs.end()) {
-          GraphEntry ge;
-          HIPC(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
-          int rc = enqueue(h->cap_stream, k, i0, i1);
-          hipGraph_t g = nullptr;
-          hipError_t ee = hipStreamEndCapture(h->cap_stream, &g);
-          if (rc != PETDIFF_OK) {
-            if (g) (void)hipGraphDestroy(g);
-            return rc;
-          }
-          HIPC(ee);
-          ge.graph = g;
-          HIPC(hipGraphInstantiate(&ge.exec, g, nullptr, nullptr, 0));
-          it = h->graphs.emplace(key, ge).first;
+    std::vector<hipGraphExec_t> ex((size_t)nseg);
+    for (int sg = 0; sg < nseg; ++sg) {
+      const int i0 = sg * seg, i1 = std::min(n_steps, i0 + seg);
+      std::vector<int> key{B, flag_var_tilde, tac ? 1 : 0, n_steps, i0, i1};
+      key.insert(key.end(), t_seq, t_seq + n_steps);
+      auto it = h->graphs.find(key);
+      if (it == h->graphs.end()) {
+        GraphEntry ge;
+        HIPC(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
+        int rc = enqueue(h->cap_stream, i0, i1);
+        hipGraph_t g = nullptr;
+        hipError_t ee = hipStreamEndCapture(h->cap_stream, &g);
+        if (rc != PETDIFF_OK) {
+          if (g) (void)hipGraphDestroy(g);
+          return rc;
         }
-        ex[(size_t)k * nseg + sg] = it->second.exec;
+        HIPC(ee);
+        ge.graph = g;
+        HIPC(hipGraphInstantiate(&ge.exec, g, nullptr, nullptr, 0));
+        it = h->graphs.emplace(key, ge).first;
       }
-    if (parts == 1) {
-      for (int sg = 0; sg < nseg; ++sg) HIPC(hipGraphLaunch(ex[sg], s));
-    } else {
-      HIPC(hipEventRecord(h->split_ev[0], s));
-      HIPC(hipStreamWaitEvent(h->split_stream, h->split_ev[0], 0));
-      for (int sg = 0; sg < nseg; ++sg) {
-        HIPC(hipGraphLaunch(ex[sg], s));
-        HIPC(hipGraphLaunch(ex[(size_t)nseg + sg], h->split_stream));
-      }
-      HIPC(hipEventRecord(h->split_ev[1], h->split_stream));
-      HIPC(hipStreamWaitEvent(s, h->split_ev[1], 0));
+      ex[sg] = it->second.exec;
     }
+    for (int sg = 0; sg < nseg; ++sg) HIPC(hipGraphLaunch(ex[sg], s));
   }
   HIPC(hipMemcpyAsync(x_out, bufs[n_steps & 1], xbytes, hipMemcpyDeviceToDevice, s));
   return PETDIFF_OK;

@@ -62,13 +62,6 @@ struct FinalArgs {
   // epilogue also runs down0 on x_next for its own samples (writing next.s0 / next.p0),
   // which removes the down0 launch from every step but the first.
   Down0Args next;
-  // Fused down1 of the NEXT reverse step (16-bit networks, with `next`): when d1_w is set the epilogue
-  // also runs down1 (Conv1D 128 -> 256, k6 + res, MaxPool) on its own samples' p0, so the down1 launch
-  // leaves every step but the first.  d1_w: down1's packed weights (wpack layout, bf16x3 chunk order).
-  const void* d1_w;
-  const float* d1_tmap;      // [T][24][256] time contribution + biases of level 1
-  const float* d1_cmap;      // [n_tac][24][256] label contribution (indexed by next.tac per sample)
-  void* d1_s1; void* d1_p1;  // [B][24][256], [B][12][256]
 };
 
 template <typename T>
@@ -96,16 +89,11 @@ struct ConvArgs {
 // x3: the bf16x3 network (T = bf16 only; activations stored as [hi | lo] rows, see DmaPlan)
 template <typename T>
 hipError_t launch_conv(int layer_kind, const ConvArgs<T>& a, hipStream_t s, bool x3 = false);
-// down2 and down3 in one launch with per-sample-block hand-off counters (PETDIFF_SEAM23 experiment);
-// seam_state: device int [ceil(B / 64) + 2], zero before the first launch, left zero by each launch
-template <typename T>
-hipError_t launch_seam23(const ConvArgs<T>& a2, const ConvArgs<T>& a3, int* seam_state, hipStream_t s, bool x3 = false);
 template <typename T>
 hipError_t launch_down0(const Down0Args& a, hipStream_t s, bool x3 = false);
 hipError_t launch_split_to_f32(const bf16* src, size_t rows, int C, float* dst, hipStream_t s);
 
-hipError_t launch_set_rng(unsigned long long* dst, unsigned long long seed, unsigned long long off0,
-                          unsigned long long off1, int parts, hipStream_t s);
+hipError_t launch_set_rng(unsigned long long* dst, unsigned long long seed, unsigned long long off, hipStream_t s);
 template <typename T>
 hipError_t launch_to_f32(const T* src, size_t n, float* dst, hipStream_t s);
 

@@ -41,155 +41,24 @@
 #ifndef FIN_EXP
 #define FIN_EXP 0
 #endif
-// fused levels: issue the map prefetches after the first ring barrier (see the fused K loop)
-#ifndef CONV_MAPS_LATE
-#define CONV_MAPS_LATE 0
-#endif
-// final 1x1 conv row loop (A/B switches, see the row loop)
-#ifndef FIN_SCALAR_W
-#define FIN_SCALAR_W 0
-#endif
-#ifndef FIN_SPLIT
-#define FIN_SPLIT 0
-#endif
 // p_sample's Box-Muller: 1 = fdlibm-form log + sincospi (philox_normal2), 0 = ocml log + sincos
 #ifndef PETDIFF_BM_FAST
 #define PETDIFF_BM_FAST 1
 #endif
-// Tap reuse in registers (fused levels whose fragments each hold ONE position of 32 samples,
-// i.e. up0): a wave's 3 fragments sit at positions 2 (segment 1) or 1 (segment 2) apart, so the
-// taps' A fragments are 10 (resp. 6) distinct LDS rows instead of 18 (12).  0 = one read per
-// (tap, fragment) as in the other layers (A/B switch).
-#ifndef CONV_TAP_REUSE
-#define CONV_TAP_REUSE 1
-#endif
-// down3 (L = 6, k = 6): a quarter of the (row, tap) products read SAME padding; down2 (L = 12): 1/8.
-// With position-major tile rows each fragment is one position of 32 samples, so a whole (fragment,
-// tap) MFMA is either useful or zero; fragments are dealt to the waves so every wave keeps 13 or 14
-// (down3) / 15 or 16 (down2) of 18 and skips the rest, and a fragment's lanes read consecutive LDS
-// rows (0 = sample-major rows, every tap multiplied).
-#ifndef CONV_DOWN3_PM
-#define CONV_DOWN3_PM 1
-#endif
-// down2 position-major (its 4 fragment sets keep 16/16/16/15 of 18): bitwise equal to sample-major;
-// down2 18.40 vs 18.64 us once the prologue's row offsets use the wave-uniform set
-// loader-wave layers: issue chunks 0, 1, 2 together at kernel start (0 = chunk 0 first, then 1 and 2
-// after it landed)
-#ifndef CONV_LDR_EARLY
-#define CONV_LDR_EARLY 0
-#endif
-// s_setprio of the MFMA waves in the loader-wave layers (0 = default arbitration)
-#ifndef CONV_MFMA_PRIO
-#define CONV_MFMA_PRIO 0
-#endif
-#ifndef CONV_DOWN2_PM
-#define CONV_DOWN2_PM 1
-#endif
-// down1 (L = 24, 16 samples per tile) pair-position-major: fragment F = positions 2F, 2F + 1 of the
-// tile's 16 samples (lanes 0-15 / 16-31), LDS input slots position-major (p * 16 + s).  A lane
-// group of 16 then reads 16 consecutive slots, or (tap outside the sample) the zero row as a
-// broadcast, instead of sample-major rows broken by zero-row substitutions (LDS bank conflicts).
-// The K walk per output row is unchanged, so the results are bitwise those of sample-major rows.
-// Measured and off: LDS bank conflicts 442 k -> 111 k (-> 307 k with the
-// sample-major C-tile remap below) per launch, but down1 14.65 vs 14.50 us, 0.9 % slower end to end.
-// up0 fused level (tap reuse path, S = 32): a fragment is one coarse row m of 32 samples, so the
-// m = 0 fragment's composite tap 0 reads coarse row -1, the zero row.  1 = the waves holding m = 0
-// run their left-edge correction MFMAs (b[0] x correction weights) in place of those zero-operand
-// tap-0 MFMAs (operands selected per wave), instead of 2 extra MFMAs per k-group: 52 -> 48 MFMAs per
-// segment-2 chunk on those waves, the same 48 as the other waves (0 = separate correction MFMAs).
-// Measured and off (profiles/r02/ab/up0_edge_tap0): up0.fused 72.40 vs 72.29 us, 4538 vs 4545
-// samples/s, 8 % more active instructions (the operand selects); not bitwise equal (the correction
-// of k-group 1 is added 4 steps later), within rounding of it.
-#ifndef CONV_UP0_EDGE_TAP0
-#define CONV_UP0_EDGE_TAP0 0
-#endif
-#ifndef CONV_DOWN1_PP
-#define CONV_DOWN1_PP 0
-#endif
-// up0 fused level, zero (fragment, tap) products skipped.  A fragment is one coarse row m of 32
-// samples (fine position l = 2m + e), so a (fragment, tap) MFMA either reads data or the zero row:
-// segment 1 (skip s2, 6 taps at l) reads padding at l = 0, 1, 9, 10, 11 (9 of 72 products),
-// segment 2 (coarse b, 4 composite taps at m) at m = 0 (tap 0, which the left-edge correction
-// covers), m = 4, 5 (3 of 24).  The waves keep their output phase e (segment 2's B taps are per
-// phase) and take the coarse rows {0, 4, 1} / {5, 2, 3}, which balances the zeros: per k-group the
-// slowest wave runs 16 of 18 segment-1 and 11 of 13 segment-2 (incl. correction) products instead
-// of 18 and 13.  Each wave runs a main loop specialised on its set (no per-step branch); the MFMA
-// order per accumulator is the tap-reuse path's, so the results are bitwise unchanged.
-// 0 = the tap-reuse path (every product, consecutive rows {0, 1, 2} / {3, 4, 5}).
-#ifndef CONV_UP0_ZS
-#define CONV_UP0_ZS 1
-#endif
-// up0 zero-skip with the A fragments cached per input position: within a k-group each position a wave's
-// (fragment, tap) pairs read is loaded from LDS once (the taps of neighbouring fragments overlap), and a
-// paired bf16x3 chunk's (a_hi, w_lo) group reuses its (a_hi, w_hi) group's A fragments.  The LDS fragment
-// reads cost the chip about as much power as the L2 -> LDS stream (conv_micro stamps: 1.95 GHz without
-// either, 1.6 with both).  0 = one read per (fragment, tap).
-#ifndef CONV_UP0_ZS_CACHE
-#define CONV_UP0_ZS_CACHE 1
-#endif
-// up0 zero-skip with 6 fragments per wave: wave w computes phase w >> 1, all 6 coarse rows (192 tile rows),
-// for output columns [32 (w & 1), +32) -- one B fragment per step for 6 MFMAs instead of two for 6, and with
-// the per-position cache 12 (6) A reads per segment-1 (-2) k-group.  LDS fragment reads per MFMA drop about
-// a quarter; the zero products per wave stay balanced (phase 0: 32 / 21, phase 1: 31 / 21 per k-group).
-#ifndef CONV_UP0_W6
-#define CONV_UP0_W6 1
-#endif
-// The same per-position A cache on the position-major down layers (down2, down3), whose fragments are also
-// one position of 32 samples: a fragment set's taps read 6-12 distinct positions instead of 13-16 (fragment,
-// tap) pairs per k-group.
-#ifndef CONV_PM_CACHE
-#define CONV_PM_CACHE 1
-#endif
-// up1.fused (16 samples per tile: a fragment is two coarse rows m, m + 1 of 16 samples): the A fragment of
-// (fragment i, tap j) equals that of (i + 1, j - 4) in segment 1 and of (i + 1, k - 2) in segment 2, so each
-// k-group reads 14 of its 18 (segment 1) and 8 of its 12 (segment 2) A fragments, cached by key 4 i + j /
-// 2 i + k; a paired bf16x3 chunk's (a_hi, w_lo) group reuses the (a_hi, w_hi) group's.  0 = every read.
-#ifndef CONV_UP1_CACHE
-#define CONV_UP1_CACHE 1
-#endif
-// down1 with the pair-position-major layout (CONV_DOWN1_PP) and the same keyed cache: fragment F holds
-// positions 2F, 2F + 1 of the tile's 16 samples, so (F, j) reads what (F + 1, j - 2) read (key 2 F + j):
-// 10 of a k-group's 18 A fragments.  Needs CONV_DOWN1_PP=1.
-#ifndef CONV_DOWN1_CACHE
-#define CONV_DOWN1_CACHE 0
-#endif
-// Final level: its 49 KB of time / label map rows go out after segment-1 chunk FIN_MAPS_KM's pieces, in the
-// middle of the K loop, instead of beside chunk 0 in the start-up burst of all 256 workgroups; the ring
-// barriers after chunks KM and KM + 1 allow them in flight (counted vmcnt), the one after KM + 2 retires them.
-#ifndef CONV_FIN_MAPS_MID
-#define CONV_FIN_MAPS_MID 0
-#endif
-#ifndef FIN_MAPS_KM
-#define FIN_MAPS_KM 2
-#endif
-// Position-major down layers with 6 fragments per wave (as CONV_UP0_W6): wave w computes fragment set w >> 1
-// (down3: all 6 positions of sample half w >> 1; down2: positions {0,2,3,10,4,5} / {1,9,6,11,7,8}) for
-// output columns [32 (w & 1), +32): one B read per 6 MFMAs, the set's input positions read once per k-group.
-#ifndef CONV_PM_W6
-#define CONV_PM_W6 1
-#endif
-
-// Issue order of a step's 6 MFMAs (fragment i, B half jn): 0 = A-major (0,0) (0,1) (1,0) (1,1) (2,0)
-// (2,1), the reads interleaved a0 b0 b1 a1 a2; 1 = B-major (0,0) (1,0) (2,0) (0,1) (1,1) (2,1), consecutive
-// MFMAs sharing their B operand, the reads a0 b0 a1 a2 b1 (in the order the next step consumes them).
-// Each accumulator still takes its MFMAs in step order, so the results are bitwise the same.
-// Measured (profiles/r03/ab/mfma_order): up2.fused 38.3-38.4 vs 39.1-39.4 us in conv_micro, the other
-// layers within noise, bench 5062-5122 vs 5045-5111 samples/s; kept.
-#ifndef CONV_MFMA_ORDER
-#define CONV_MFMA_ORDER 1
-#endif
-#define PETDIFF_CALL(m, a) m a
-#if CONV_MFMA_ORDER
-#define PETDIFF_O1 (1, 0)
-#define PETDIFF_O2 (2, 0)
-#define PETDIFF_O3 (0, 1)
-#define PETDIFF_O4 (1, 1)
-#else
-#define PETDIFF_O1 (0, 1)
-#define PETDIFF_O2 (1, 0)
-#define PETDIFF_O3 (1, 1)
-#define PETDIFF_O4 (2, 0)
-#endif
+// Layer-specific K loops (each was A/B-measured against its predecessor, which the
+// history keeps; profiles/r0*/ab/):
+//  * down2 / down3, position-major tiles: a 32-row fragment is ONE position of 32 samples, so a (fragment,
+//    tap) MFMA is wholly useful or wholly SAME padding; the zero ones are dropped at compile time.  Wave w
+//    computes fragment set w >> 1 (down3: the 6 positions of sample half w >> 1; down2: positions
+//    {0,2,3,10,4,5} / {1,9,6,11,7,8}) for output columns [32 (w & 1), +32): one B read per 6 MFMAs, and
+//    each input position the set's taps read is loaded from LDS once per k-group (zap[half][position]).
+//  * up0.fused, the same idea on the coarse rows: wave w computes output phase w >> 1, all 6 coarse rows,
+//    for columns [32 (w & 1), +32), zero products skipped, A cached per input position.
+//  * up1.fused (16 samples per tile, a fragment is coarse rows m, m + 1): the A fragment of (i, j) equals
+//    that of (i + 1, j - 4) (segment 1) / (i + 1, k - 2) (segment 2), cached by key.
+//  * everything else (down1, up2.fused, the unfused / f16 / f32 paths): one read per (fragment, tap).
+// A step's MFMAs go out B-major, (0,0) (1,0) (2,0) (0,1) (1,1) (2,1), so consecutive MFMAs share their B
+// operand; every accumulator takes its MFMAs in step order.
 
 namespace petdiff {
 
@@ -375,14 +244,10 @@ struct ConvGeom {
   static constexpr int WM = TC.wm, WN = TC.wn, STAGES = TC.stages, ROWB = TC.rowb;
   static constexpr int MT = 96 * WM, NT = 64 * WN;
   static constexpr int S = MT / L;                  // samples per workgroup
-  // Position-major down layers (CONV_DOWN3_PM, CONV_DOWN2_PM): wave w's fragment i is position
-  // pm_pos(w / SH, i) of samples 32 (w % SH) .. +31 (SH = sample halves per tile).
-  //   down3 (L = 6, S = 64): {2, 0, 5} keep 13 of the 18 (fragment, tap) products, {3, 1, 4} 14.
-  //   down2 (L = 12, S = 32): {0, 2, 3}, {10, 4, 5}, {1, 9, 6} keep 16, {11, 7, 8} 15.
-  static constexpr bool PM = sizeof(T) == 2 && ((CONV_DOWN3_PM && KIND == LK_DOWN3) ||
-                                                (CONV_DOWN2_PM && KIND == LK_DOWN2));
-  static constexpr bool PP = sizeof(T) == 2 && CONV_DOWN1_PP && KIND == LK_DOWN1;
-  static constexpr bool POSMAJ = PM || PP;          // LDS input slots p * S + s
+  // Position-major down layers (down2, down3): LDS input slots p * S + s, and tile row block
+  // (pat, sample half) holds positions pm_pos(pat, 0..2) of 32 samples (SH = sample halves per tile);
+  // the epilogue's row order.  The K loop deals positions to the waves by pw6_pos.
+  static constexpr bool PM = sizeof(T) == 2 && (KIND == LK_DOWN3 || KIND == LK_DOWN2);
   static constexpr int SH = PM ? S / 32 : 1;        // sample halves (waves per fragment set)
   static constexpr int NPAT = 4 / SH;               // fragment sets
   // fragment set pat, fragment i -> position, packed 4 bits per entry (index 3 pat + i), so a
@@ -391,18 +256,7 @@ struct ConvGeom {
   static constexpr __device__ __host__ int pm_pos(int pat, int i) {
     return (int)((PM_TAB >> (4 * (3 * pat + i))) & 15);
   }
-  static constexpr __device__ __host__ bool pm_valid(int pat, int i, int j) {
-    return pm_pos(pat, i) + j - PADL >= 0 && pm_pos(pat, i) + j - PADL < L;
-  }
-  // (fragment i, tap j) is the first pair of set pat, in tap order, to read its input position
-  static constexpr __device__ __host__ bool pm_first(int pat, int i, int j) {
-    for (int j2 = 0; j2 < j; ++j2)
-      for (int i2 = 0; i2 < 3; ++i2)
-        if (pm_valid(pat, i2, j2) && pm_pos(pat, i2) + j2 == pm_pos(pat, i) + j) return false;
-    return true;
-  }
-  // CONV_PM_W6: fragment f (0..5) of set `set` is position pw6_pos of sample half pw6_sh
-  static constexpr bool PW6 = PM && CONV_PM_CACHE && CONV_PM_W6;
+  // fragment f (0..5) of set `set` (waves 2 set, 2 set + 1) is position pw6_pos of sample half pw6_sh
   static constexpr __device__ __host__ int pw6_pos(int set, int f) {
     return L == 6 ? f
                   : set == 0 ? (f == 0 ? 0 : f == 1 ? 2 : f == 2 ? 3 : f == 3 ? 10 : f == 4 ? 4 : 5)
@@ -462,39 +316,12 @@ struct ConvGeom {
   static constexpr bool AFULL2 = true;
   static constexpr int PER2 = APT2 + BPT2;          // segment-2 chunks
   static constexpr int PHROWS = FUSED ? S * LH : MT; // tile rows per output phase (fused)
-  // up0 zero-skip (CONV_UP0_ZS): wave wm computes phase wm >> 1, coarse rows zs_m(wm & 1, i)
-  static constexpr bool ZS = CONV_UP0_ZS && FUSED && S == 32 && L == 12 && sizeof(T) == 2 && STAGES == 3;
-  static constexpr __device__ __host__ int zs_m(int set, int i) {
-    return set == 0 ? (i == 0 ? 0 : i == 1 ? 4 : 1) : (i == 0 ? 5 : i == 1 ? 2 : 3);
-  }
-  // (fragment i, segment-1 tap j) / (fragment i, composite tap k) of wave pat reads data
-  static constexpr __device__ __host__ bool zs_valid1(int pat, int i, int j) {
-    return 2 * zs_m(pat & 1, i) + (pat >> 1) + j - PADL >= 0 && 2 * zs_m(pat & 1, i) + (pat >> 1) + j - PADL < L;
-  }
-  static constexpr __device__ __host__ bool zs_valid2(int pat, int i, int k) {
-    return zs_m(pat & 1, i) - 1 + k >= 0 && zs_m(pat & 1, i) - 1 + k < LH;
-  }
-  // segment seg's tap order (segment 1: 0 2 4 1 3 5), the input position (fine l or coarse q) that
-  // fragment i of wave pat reads at tap j, and whether tap order index jj is the first in a k-group to read it
+  // up0.fused (W6): wave w computes output phase e = w >> 1, its fragment f (0..5) is coarse row m = f
+  // (fine position l = 2 m + e) of the tile's 32 samples; segment seg's tap order (segment 1: 0 2 4 1 3 5)
+  static constexpr bool W6 = FUSED && S == 32 && L == 12 && sizeof(T) == 2 && STAGES == 3;
   static constexpr __device__ __host__ int zs_tap(int seg, int jj) {
     return seg == 2 ? jj : (jj < 3 ? 2 * jj : 2 * (jj - 3) + 1);
   }
-  static constexpr __device__ __host__ int zs_pos(int seg, int pat, int i, int j) {
-    return seg == 2 ? zs_m(pat & 1, i) - 1 + j : 2 * zs_m(pat & 1, i) + (pat >> 1) + j - PADL;
-  }
-  static constexpr __device__ __host__ bool zs_ok(int seg, int pat, int i, int j) {
-    return seg == 2 ? zs_valid2(pat, i, j) : zs_valid1(pat, i, j);
-  }
-  static constexpr __device__ __host__ bool zs_first(int seg, int pat, int i, int jj) {
-    for (int j2 = 0; j2 < jj; ++j2)
-      for (int i2 = 0; i2 < 3; ++i2)
-        if (zs_ok(seg, pat, i2, zs_tap(seg, j2)) &&
-            zs_pos(seg, pat, i2, zs_tap(seg, j2)) == zs_pos(seg, pat, i, zs_tap(seg, jj)))
-          return false;
-    return true;
-  }
-  // CONV_UP0_W6: fragment f (0..5) of a phase-e wave is coarse row m = f
-  static constexpr bool W6 = ZS && CONV_UP0_ZS_CACHE && CONV_UP0_W6;
   static constexpr __device__ __host__ int w6_pos(int seg, int e, int f, int j) {
     return seg == 2 ? f - 1 + j : 2 * f + e + j - PADL;
   }
@@ -508,11 +335,8 @@ struct ConvGeom {
           return false;
     return true;
   }
-  // first tile row of wave wm's fragment i (tile rows stay [phase][m][sample] for the epilogue)
-  static __device__ __forceinline__ int frag_row(int wm, int i) {
-    if constexpr (ZS) return (wm >> 1) * PHROWS + zs_m(wm & 1, i) * S;
-    else return wm * 96 + i * 32;
-  }
+  // first tile row of wave wm's fragment i
+  static __device__ __forceinline__ int frag_row(int wm, int i) { return wm * 96 + i * 32; }
   static constexpr int CT_LD = 2 * NT + 8;          // fp32 C tile, one ROW PAIR [c][2] per line (non-final)
   static constexpr int FIN_LD = 132;                // fp32 C tile row (final epilogue, 16-B aligned)
   // FINAL: C tile | final kernel [128][4] | x_next rows [MT][2] (fused next-step down0)
@@ -559,8 +383,6 @@ struct ConvGeom {
                 "position-major layout: 3 positions of 32 samples per wave");
   static_assert(!PM || (CONV_LOADERS && STAGES == 3), "position-major layers run on the loader-wave ring");
   static_assert(MT % L == 0, "tile must hold whole samples");
-  static_assert(!PP || (S == 16 && L % 2 == 0 && MT == 32 * (L / 2) && !UPS && !FUSED && EPI == EPI_POOL),
-                "pair-position-major: a fragment is two positions of 16 samples");
   static_assert(B_BYTES % (16 * kThreads) == 0, "B tile split");
   static_assert(ROWB == 64 || ROWB == 128 || (ROWB == 32 && FUSED), "row width");
   static_assert(STAGES == 2 || (STAGES == 3 && AFULL && AFULL2), "3-stage ring needs uniform per-wave DMA counts");
@@ -682,9 +504,9 @@ struct DmaPlan {
       const int c = cp ^ G::key(row);
       // LDS row: (sample, position) = row / LIN, row % LIN; fused: position-major slots
       // (row = li * S + s), so a lane group's 16 samples read 16 consecutive rows
-      const int s = (G::FUSED || G::POSMAJ) ? row % G::S : row / G::LIN;
+      const int s = (G::FUSED || G::PM) ? row % G::S : row / G::LIN;
       const int q1 = row / G::S;                 // fused: slot1 position index
-      const int li = G::FUSED ? (q1 < G::LH ? 2 * q1 : 2 * (q1 - G::LH) + 1) : G::POSMAJ ? q1 : row - s * G::LIN;
+      const int li = G::FUSED ? (q1 < G::LH ? 2 * q1 : 2 * (q1 - G::LH) + 1) : G::PM ? q1 : row - s * G::LIN;
       const int b = min(m0 + s, a.B - 1);        // rows of absent samples only feed unstored outputs
       avoff1[qq] = ((b * G::LIN + li) * RS * a.c1 + pcol(c, a.c1)) * (int)sizeof(T);
       avoff2[qq] = ((b * G::LIN + li) * RS * a.c2 + pcol(c, a.c2)) * (int)sizeof(T);
@@ -779,34 +601,6 @@ struct DmaPlan {
   }
 };
 
-// Fused down1 of the next reverse step, run by the final level's 4 waves on the tile's 4 samples:
-// relu(conv6(p0) + conv1(p0) + maps) -> s1 and MaxPool -> p1 (networks.py:589-711), as the
-// standalone conv_kernel<down1> computes it -- the same bf16 operands and fp32 MFMA accumulation
-// order (chunk of 32 channels, tap, k-group of 16), so the results are bitwise equal.  Wave w owns
-// output channels [64 w, 64 w + 64) (N-tile w of down1's packed weights); its B fragments stream
-// from L2 through a 4-deep register ring, its A fragments come from the p0 rows in LDS.
-// Fused down1 (FinalArgs::d1_w) tile in the final level's LDS, after the down0 map rows [48][128] f32:
-// A = p0 rows of the tile's samples [4 x 24 + zero row][128] bf16 (272-B rows: a 16-lane group's
-// ds_read_b128 covers all 64 banks), then the level-1 map rows [24][256] f32 (time + label + biases).
-// bf16x3 (XS = 1): a p0 row is [hi(128) | lo(128)] (528-B rows, the same 4-dword bank shift per row).
-// A tile with more than one condition (per-sample tac) reads its level-1 map rows from L2 in the epilogue.
-template <int XS> struct D1L {
-  static constexpr int Ldb = XS ? 528 : 272, A = 48 * 128 * 4, Rows = 4 * 24, M = A + (Rows + 1) * Ldb;
-  static constexpr int MAPB = 24 * 256 * 4;
-  // B ring: a B unit = one (chunk, tap) of all 4 N-tiles = 4 x 4 KB; slots from the end of the map
-  // rows to the end of the final level's LDS (bf16x3: 3 there + one in the dead down0-map rows)
-  static constexpr int UNIT = 4 * 4096, SLOT0 = (M + MAPB + 255) / 256 * 256;
-  static constexpr int NS_HI = (162560 - SLOT0) / UNIT;
-  static constexpr int NS = NS_HI >= 5 ? 5 : NS_HI + 1;
-  static_assert(NS * 4096 >= (XS ? 12288 : 18432), "wave-private staging of the s1 / p1 rows");
-  static constexpr __host__ __device__ int slot_off(int s) { return s < NS_HI ? SLOT0 + s * UNIT : 0; }
-};
-
-// diagnostic builds of the fused down1 (FD1_DIAG): 2 = no MFMAs, 4 = no B DMA after the first units
-// (stale B), 8 = no staging / stores (beware: the compiler then drops the MFMAs of the unused accumulators)
-#ifndef FD1_DIAG
-#define FD1_DIAG 0
-#endif
 template <typename T> __device__ __forceinline__ T to_t(float v);
 template <> __device__ __forceinline__ bf16 to_t<bf16>(float v) { return (bf16)v; }
 template <> __device__ __forceinline__ f16 to_t<f16>(float v) { return (f16)v; }
@@ -894,204 +688,12 @@ __device__ __forceinline__ void store_act(T* base, size_t row, int C, int n, con
   else Vec8<T>::store(base + row * C + n, v);
 }
 
-// Fused down1 of the next reverse step (FinalArgs::d1_w), run by the final level's 4 waves on the tile's 4
-// samples: relu(conv6(p0) + conv1(p0) + maps) -> s1 and MaxPool -> p1 (networks.py:589-711), with the
-// standalone conv_kernel<down1>'s operands and fp32 MFMA accumulation order (chunk of 32 channels, tap,
-// k-group of 16): bitwise equal.  Wave w owns output channels [64 w, 64 w + 64) (N-tile w of down1's
-// packed weights).  A = the p0 rows in LDS (written by the fused down0), read one step ahead.  B: every
-// wave copies its own 4 KB of unit u + D (unit = one (chunk, tap)) into a ring slot by LDS-DMA
-// (buffer_load ... lds, 4 instructions per lane, a fixed count per unit so every vmcnt wait is one
-// constant; the units past the last are out-of-range reads that land zeros in dead slots), and reads unit
-// u + 1's fragments while the MFMAs of unit u run; one s_barrier per unit.  The outputs leave as 16-B
-// stores through wave-private staging in the ring.
-// Measured (profiles/r03/fused_down1): about 12.8 us inside up2 (K loop 8.0 at ~47
-// cycles per MFMA, epilogue + drain 4.8) against 16-17 us for the standalone launch with its boundary,
-// which is a wash end to end: each workgroup streams all 393 KB of down1's weights for 4 samples (the
-// standalone tile reuses its 98 KB over 16).  Off by default; PETDIFF_FUSE_DOWN1=1 turns it on.
-template <typename T, int XS, bool MIXED, typename FA>
-__device__ __forceinline__ void fused_down1_lds(const FA& f, char* smem, int m0, int nb, int w, int lane, int t_next,
-                                                const int* tac_next, int B) {
-  typedef typename Frag<T>::type fragT;
-  using DL = D1L<XS>;
-  constexpr int NTD = 64, NCH = XS ? 12 : 4, NU = 6 * NCH, NS = DL::NS, D = NS - 1;
-  static_assert(NS >= 3 && D - 2 >= 0 && 4 * (D - 2) < 64, "ring depth");
-  const int lr = lane & 31, h = lane >> 5;
-  int aoff[6][3];
-#pragma unroll
-  for (int j = 0; j < 6; ++j)
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int r = i * 32 + lr, sm = r / 24, l = r - 24 * sm, p = l + j - 2;
-      const int row = (p >= 0 && p < 24) ? sm * 24 + p : DL::Rows;
-      aoff[j][i] = DL::A + row * DL::Ldb + h * 16;
-    }
-  int boff[2][2];
-#pragma unroll
-  for (int g = 0; g < 2; ++g)
-#pragma unroll
-    for (int jn = 0; jn < 2; ++jn) {
-      const int n = jn * 32 + lr;
-      boff[g][jn] = w * 4096 + ((n * 64 + ((h ^ ((n >> 2) & 3)) << 4)) ^ (g << 5));
-    }
-  constexpr int TILE = NCH * 6 * 4096;
-  const i32x4 rsw = make_rsrc(f.d1_w, 4u * (unsigned)TILE);
-  // unit u of this wave: its 4 KB at w * TILE + u * 4096 (chunk u / 6, tap u % 6 are consecutive)
-  auto issue = [&](int u) {
-    char* dst = smem + DL::slot_off(u % NS) + w * 4096;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int off = u < NU ? w * TILE + u * 4096 + k * 1024 + lane * 16 : 0x7ffffff0;   // past the end: zeros
-      llvm_amdgcn_raw_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(dst + k * 1024), 16, off, 0, 0, 0);
-    }
-  };
-  f32x16 acc[3][2];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int jn = 0; jn < 2; ++jn)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][jn][e] = 0.f;
-#pragma unroll
-  for (int u = 0; u < D; ++u) issue(u);
-  auto ldb = [&](int u, fragT (&dst)[2][2]) {
-    const char* base = smem + DL::slot_off(u % NS);
-#pragma unroll
-    for (int g = 0; g < 2; ++g)
-#pragma unroll
-      for (int jn = 0; jn < 2; ++jn) dst[g][jn] = *reinterpret_cast<const fragT*>(base + boff[g][jn]);
-  };
-  auto lda = [&](int st, fragT (&dst)[3]) {
-    const int u = st >> 1, g = st & 1, kc = u / 6, j = u % 6;
-    const int cb = (kc & 3) * 64 + (XS && kc >= 8 ? 256 : 0);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) dst[i] = *reinterpret_cast<const fragT*>(smem + aoff[j][i] + cb + g * 32);
-  };
-  fragT bv[2][2][2], av[2][3];
-  wait_vmcnt<4 * (D - 1)>();                     // unit 0 landed (own DMA)
-  ring_barrier<4 * (D - 1)>();                   // ... for every wave
-  ldb(0, bv[0]);
-  lda(0, av[0]);
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int u = 0; u < NU; ++u) {
-    // unit u + 1 landed for every wave; every wave is done reading slot (u - 1) % NS = (u + D) % NS
-    ring_barrier<4 * (D - 2)>();
-    if constexpr (!(FD1_DIAG & 4)) issue(u + D);
-    else if (u == 0) { issue(u + D); issue(u + D + 1); issue(u + D + 2); }   // diag: the counts stay valid
-    if (u + 1 < NU) ldb(u + 1, bv[(u + 1) & 1]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      const int st = 2 * u + g;
-      if (st + 1 < 2 * NU) lda(st + 1, av[(st + 1) & 1]);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int jn = 0; jn < 2; ++jn) {
-          if constexpr (FD1_DIAG & 2) acc[i][jn][0] += (float)av[st & 1][i][0] * (float)bv[u & 1][g][jn][0];
-          else acc[i][jn] = mfma32(av[st & 1][i], bv[u & 1][g][jn], acc[i][jn]);
-        }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  wait_vmcnt<0>();                               // the dummy units are out of the LDS before it is reused
-#if CONV_EXP_MODE & 128
-  if (threadIdx.x == 0) reinterpret_cast<unsigned long long*>(f.x_all)[7168 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-#endif
-  T* s1 = reinterpret_cast<T*>(f.d1_s1);
-  T* p1 = reinterpret_cast<T*>(f.d1_p1);
-  const float* tm1 = f.d1_tmap + (size_t)t_next * 24 * 256;
-  // relu(acc + maps) in place: accumulator rows (e, e + 1) are positions (l, l + 1) of one sample
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int jn = 0; jn < 2; ++jn) {
-      const int n = w * NTD + jn * 32 + lr;
-#pragma unroll
-      for (int e = 0; e < 16; e += 2) {
-        const int r = i * 32 + 8 * (e >> 2) + 4 * h + (e & 3);
-        const int sm = r / 24, l = r - 24 * sm;
-        float m0v, m1v;
-        if constexpr (MIXED) {   // time + this sample's label rows from L2 (tmap + cmap, the standalone order)
-          const int tac_s = tac_next ? tac_next[min(m0 + sm, B - 1)] : 0;
-          const float* cm1 = f.d1_cmap + (size_t)tac_s * 24 * 256;
-          m0v = tm1[l * 256 + n] + cm1[l * 256 + n];
-          m1v = tm1[(l + 1) * 256 + n] + cm1[(l + 1) * 256 + n];
-        } else {
-          const float* md = reinterpret_cast<const float*>(smem + DL::M);
-          m0v = md[l * 256 + n];
-          m1v = md[(l + 1) * 256 + n];
-        }
-        acc[i][jn][e] = fmaxf(acc[i][jn][e] + m0v, 0.f);
-        acc[i][jn][e + 1] = fmaxf(acc[i][jn][e + 1] + m1v, 0.f);
-      }
-    }
-  // The s1 / p1 rows leave as 16-B stores of 8 channels (one 2-B store per value and lane had kept the
-  // fused down1 at ~12 us, most of it draining 73 KB per workgroup of 2-B writes): each wave stages its
-  // [96][64] s1 and [48][64] pooled p1 slices as 16-bit rows in its OWN 4-KB parts of the ring slots
-  // (written only by this wave's DMAs, all landed: no barrier), then reads back 16-B pieces.
-  // bf16x3 rows are [hi(256) | lo(256)]: one plane per round (16 KB of private staging).
-  auto stg = [&](int q) -> char* { return smem + DL::slot_off(q >> 12) + w * 4096 + (q & 4095); };
-  auto put = [&](int q, float v, int pl) {
-    const T hi = to_t<T>(v);
-    *reinterpret_cast<T*>(stg(q)) = pl ? to_t<T>(v - (float)hi) : hi;
-  };
-  auto put_s1 = [&](int pl) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int jn = 0; jn < 2; ++jn)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) put((i * 32 + 8 * (e >> 2) + 4 * h + (e & 3)) * 128 + (jn * 32 + lr) * 2,
-                                         acc[i][jn][e], pl);
-  };
-  auto put_p1 = [&](int q0, int pl) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int jn = 0; jn < 2; ++jn)
-#pragma unroll
-        for (int e = 0; e < 16; e += 2)
-          put(q0 + ((i * 32 + 8 * (e >> 2) + 4 * h + (e & 3)) >> 1) * 128 + (jn * 32 + lr) * 2,
-              fmaxf(acc[i][jn][e], acc[i][jn][e + 1]), pl);
-  };
-  // rows [0, nrows) of 128 B at staging offset q0 -> global rows of tensor `base` (L positions per sample)
-  auto flush = [&](T* base, int nrows, int L_, int q0, int pl) {
-    for (int k = 0; k < nrows / 8; ++k) {
-      const int pc = k * 64 + lane, r = pc >> 3, c = pc & 7, sm = r / L_, l = r - sm * L_;
-      if (sm < nb) {
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(stg(q0 + r * 128 + c * 16));
-        T* dst = base + ((size_t)(m0 + sm) * L_ + l) * (XS ? 512 : 256) + pl * 256 + w * NTD + c * 8;
-        store16(reinterpret_cast<bf16x8*>(dst), v);
-      }
-    }
-  };
-  if constexpr (FD1_DIAG & 8) {   // diagnostic: no staging / stores (one guarded store keeps the values live)
-    if (acc[0][0][0] == 12345.f && acc[2][1][15] == 54321.f) s1[lane] = (T)1.f;
-  } else if constexpr (XS == 0) {
-    put_s1(0);
-    put_p1(96 * 128, 0);
-    flush(s1, 96, 24, 0, 0);
-    flush(p1, 48, 12, 96 * 128, 0);
-  } else {
-    put_s1(0);
-    flush(s1, 96, 24, 0, 0);
-    put_s1(1);
-    flush(s1, 96, 24, 0, 1);
-    put_p1(0, 0);
-    put_p1(48 * 128, 1);
-    flush(p1, 48, 12, 0, 0);
-    flush(p1, 48, 12, 48 * 128, 1);
-  }
-}
-
 // down0 positions pos0, pos0 + pstride, ... of samples b0 .. b0 + nb - 1: x from LDS
 // (xs [nb][96]), maps from LDS (mp [48][128], fast) or global, weights in registers.
 template <typename T, int XS = 0>
 __device__ __forceinline__ void down0_positions(const Down0Args& a, const float* xs, const float* mp, bool fast,
                                                 int b0, int nb, const f32x4 (&wr)[12][2], int n0, int pos0,
-                                                int pstride, char* p0l = nullptr) {
+                                                int pstride) {
   for (int pos = pos0; pos < nb * 24; pos += pstride) {
     const int bl = pos / 24, lp = pos - bl * 24, b = b0 + bl;
     const int l0 = 2 * lp;
@@ -1139,43 +741,10 @@ __device__ __forceinline__ void down0_positions(const Down0Args& a, const float*
     float pv[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) pv[q] = fmaxf(v[0][q], v[1][q]);
-    // p0 feeds only down1: with the fused down1 (p0l) it stays in LDS, no global copy
-    if constexpr (!(FIN_EXP & 2)) { if (!p0l) store_act<T, XS>(reinterpret_cast<T*>(a.p0), (size_t)b * 24 + lp, 128, n0, pv); }
+    if constexpr (!(FIN_EXP & 2)) store_act<T, XS>(reinterpret_cast<T*>(a.p0), (size_t)b * 24 + lp, 128, n0, pv);
     else if (pv[0] == 12345.f) reinterpret_cast<T*>(a.p0)[0] = (T)0.f;
-    if constexpr (sizeof(T) == 2) {
-      if (p0l) {   // fused down1: the same 16-bit row, LDS row bl * 24 + lp (D1L<XS>::Ldb bytes per row)
-        typename Frag<T>::type o, r;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          o[q] = (T)pv[q];
-          r[q] = (T)(pv[q] - (float)o[q]);      // bf16x3: the lo half (Vec8::store_split)
-        }
-        char* row = p0l + (bl * 24 + lp) * D1L<XS>::Ldb;
-        *reinterpret_cast<typename Frag<T>::type*>(row + n0 * 2) = o;
-        if constexpr (XS != 0) *reinterpret_cast<typename Frag<T>::type*>(row + (128 + n0) * 2) = r;
-      }
-    }
   }
 }
-
-// In-launch seam between two conv layers (PETDIFF_SEAM23, an experiment: DESIGN.md section 8).  Roles by
-// block index: blocks [0, n_prod) run the producer layer's tiles, the rest the consumer layer's.  A
-// producer tile, once every storing wave has drained its write-through (sc1) stores, adds 1 to the
-// counter of the consumer sample block it feeds; a consumer tile issues its first chunk's weight DMA,
-// then lane 0 of loader wave 0 polls its sample block's counter (sc1 loads, s_sleep, a bounded spin that
-// records a give-up in err instead of hanging), that wave takes the agent-scope acquire (one L1 invalidate
-// per CU), a workgroup barrier releases the other waves, and only then is the activation DMA issued.  The last consumer to finish zeroes the counters for the next launch.
-struct SeamArgs {
-  int* grp = nullptr;        // [consumer sample blocks] producer tiles done
-  int* done = nullptr;       // consumer tiles done (the last one resets grp and done)
-  int* err = nullptr;        // spins given up (0 in a correct run)
-  int n_prod = 0;            // producer tiles (= consumer block index offset)
-  int n_cons = 0;            // consumer tiles
-  int n_grp = 0;             // consumer sample blocks
-  int per_grp = 0;           // producer tiles per full sample block
-  int n_prod_m = 0;          // producer M tiles (the last sample block may have fewer)
-  int prod_n = 0;            // producer N tiles
-};
 
 // compile-time loop: f(integral_constant<int, I>) for I in [I0, N) (the step index of a fully unrolled main
 // loop whose register-array indices must fold; a #pragma unroll the compiler declines leaves them dynamic,
@@ -1193,8 +762,8 @@ __device__ __forceinline__ void static_for(F&& f) {
 template <bool P3> __device__ __forceinline__ constexpr int kg_a(int g) { return P3 ? (g == 2 ? 32 : 0) : g << 5; }
 template <bool P3> __device__ __forceinline__ constexpr int kg_b(int g) { return P3 ? (g == 1 ? 32 : 0) : g << 5; }
 
-template <typename T, int KIND, int XS, int SEAM>
-__device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int bid, const SeamArgs sa) {
+template <typename T, int KIND, int XS>
+__device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int bid) {
   using G = ConvGeom<T, KIND>;
   constexpr int L = G::L, TAPS = G::TAPS, PADL = G::PADL, EPI = G::EPI, ROWB = G::ROWB, NT = G::NT;
   constexpr bool UPS = G::UPS;
@@ -1221,30 +790,10 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   const int nN = a.cout / NT;
   const int total = nM * nN;
   const int xcd = bid & 7, loc = bid >> 3, q8 = total >> 3, r8 = total & 7;
-#ifndef CONV_XCD_MAP
-#define CONV_XCD_MAP 1    // 0: identity, 1: XCD-contiguous slots N-fastest, 2: XCD-contiguous slots M-fastest,
-                          // 3: a (bm x 4) block of the tile grid per XCD when the grid splits evenly, else 1
-                          //    (A/B: 4257/4266 vs 4295/4303 samples/s for 1, so 1 stays)
-#endif
-#if CONV_XCD_MAP == 0
-  const int slot = bid;
-#else
+  // (a per-XCD block of the tile grid, which cuts the weight traffic through each L2 by 20-30 %, measured
+  // 0.8 % slower end to end: DESIGN.md section 3)
   const int slot = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
-#endif
-#if CONV_XCD_MAP == 2
-  const int n_tile = slot / nM, m_tile = slot - n_tile * nM;
-#elif CONV_XCD_MAP == 3
-  // per XCD: bn = min(nN, 4) N tiles x bm = total / 8 / bn M tiles, so its L2 holds a few
-  // M tiles' activations and a few N tiles' weights (down3, up0: 8 x 4 instead of 2 x 16 /
-  // 4 x 8, about 20-30% less weight traffic through the XCD's L2)
-  const int bn = nN < 4 ? nN : 4, per = total >> 3, bm = per / bn;
-  const bool blk = r8 == 0 && per % bn == 0 && nN % bn == 0 && nM % bm == 0;
-  const int ncb = nN / bn;
-  const int m_tile = blk ? (xcd / ncb) * bm + loc / bn : slot / nN;
-  const int n_tile = blk ? (xcd % ncb) * bn + loc % bn : slot - (slot / nN) * nN;
-#else
   const int m_tile = slot / nN, n_tile = slot - m_tile * nN;
-#endif
   const int m0 = m_tile * G::S;
 
   constexpr bool P3 = DmaPlan<T, KIND, XS>::P3;     // paired bf16x3 chunks (x3_paired)
@@ -1294,28 +843,18 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   // per-lane LDS byte offsets of the A fragment rows (tap j, m-subtile i) and B rows
   const int c0 = (sizeof(T) == 2) ? h : 2 * h;
   const int wv = __builtin_amdgcn_readfirstlane(w);
-  const int pm_pat = wv / G::SH;                    // position-major: this wave's fragment set
-  const int wmu = G::ZS ? wv / G::WN : wm;          // up0 zero-skip: the fragment set from the uniform index
   int aoff[TAPS][3];
 #pragma unroll
   for (int j = 0; j < TAPS; ++j) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      const int r = G::frag_row(wmu, i) + lr;
+      const int r = G::frag_row(wm, i) + lr;
       int s, l;
-      if constexpr (G::PM) {   // wave-uniform position: scalar work, no divergent select chain
-        l = G::pm_pos(pm_pat, i);
-        s = (wv % G::SH) * 32 + lr;
-      } else if constexpr (G::PP) {   // fragment rows: positions 2F (lanes 0-15), 2F + 1 (16-31)
-        l = 2 * (r >> 5) + ((r >> 4) & 1);
-        s = r & 15;
-      } else {
-        G::row_sl(r, s, l);
-      }
+      G::row_sl(r, s, l);
       const int p = l + j - PADL;
       int row;
       if (G::FUSED) row = (p >= 0 && p < L) ? G::slot1(p, s) : G::ZROW;
-      else if (!UPS) row = (p >= 0 && p < L) ? (G::POSMAJ ? p * G::S + s : s * L + p) : G::ZROW;
+      else if (!UPS) row = (p >= 0 && p < L) ? (G::PM ? p * G::S + s : s * L + p) : G::ZROW;
       else row = (p < L) ? s * G::LIN + (p >> 1) : G::ZROW;
       aoff[j][i] = (G::FUSED && row == G::ZROW) ? G::ZOFF + (c0 << 4) : row * ROWB + ((c0 ^ G::key(row)) << 4);
     }
@@ -1338,14 +877,14 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     for (int k = 0; k < G::TAPS2; ++k) {
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
-        const int r = G::frag_row(wmu, i) + lr;
+        const int r = G::frag_row(wm, i) + lr;
         const int sq = r % G::S, m = (r / G::S) % G::LH, q = m - 1 + k;
         const int row = q * G::S + sq;
         aoff2[k][i] = (q >= 0 && q < G::LH) ? row * ROWB + ((c0 ^ G::key(row)) << 4) : G::ZOFF + (c0 << 4);
       }
     }
     {
-      const int r = G::frag_row(wmu, 0) + lr;
+      const int r = G::frag_row(wm, 0) + lr;
       const int sq = r % G::S, m = (r / G::S) % G::LH, row = sq;
       amask = m == 0 ? row * ROWB + ((c0 ^ G::key(row)) << 4) : G::ZOFF + (c0 << 4);
     }
@@ -1355,7 +894,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       boff2[jn] = G::A2_BYTES + (ph * G::TAPS2 * NT + n) * ROWB + ((c0 ^ G::key(n)) << 4);
     }
   }
-  // CONV_UP0_W6: wave = (phase w6e, column half w6h); A offsets per input position of the lane's sample
+  // up0.fused (W6): wave = (phase w6e, column half w6h); A offsets per input position of the lane's sample
   const int w6e = wv >> 1, w6h = wv & 1;
   constexpr int W6P1 = G::W6 ? G::L : 1, W6P2 = G::W6 ? G::LH : 1;
   int apos1[W6P1], apos2[W6P2];
@@ -1375,11 +914,11 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     }
     amask = apos2[0];
   }
-  // CONV_PM_W6: wave = (fragment set pw6set, column half w6h); A offsets per input position
+  // position-major: wave = (fragment set pw6set, column half w6h); A offsets per input position
   const int pw6set = wv >> 1;
-  constexpr int PW6P = G::PW6 ? G::L : 1;
+  constexpr int PW6P = G::PM ? G::L : 1;
   int apm[PW6P];
-  if constexpr (G::PW6) {
+  if constexpr (G::PM) {
     const int n = w6h * 32 + lr;
     boff[0] = G::A_BYTES + n * ROWB + ((c0 ^ G::key(n)) << 4);
     const int sm = (pw6set & (G::L == 6 ? 1 : 0)) * 32 + lr;   // sample of this lane (down3: half pw6set)
@@ -1423,21 +962,12 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       bv[0][1][e] = bv[1][0][e] = (std::remove_reference_t<decltype(bv[0][0][0])>)(0.02f * (lane - e));
     }
   }
-  // Tap reuse (CONV_TAP_REUSE): this wave's fragment i at tap j reads fine position P = 2i + j
-  // (segment 1) or coarse row Q = i + k (segment 2) relative to its first fragment; each step
-  // reads only the positions no earlier step of its k-group has read.  cav carries the last
-  // step's A operands into the next chunk's first step (whose MFMAs they are).
-  constexpr bool REUSE = CONV_TAP_REUSE && G::FUSED && G::S == 32 && sizeof(T) == 2 && !G::ZS && !P3;
-  fragT cav[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) cav[i] = fragT{};
-  // up0 zero-skip with cached A fragments: [32-B half][input position] (CONV_UP0_ZS_CACHE)
-  constexpr bool ZAP = (G::ZS && CONV_UP0_ZS_CACHE) || (G::PM && CONV_PM_CACHE);
+  // up0.fused / position-major A fragments cached per input position: [32-B half][input position]
+  constexpr bool ZAP = G::W6 || G::PM;
   constexpr int ZAP_H = ZAP ? 2 : 1, ZAP_P = ZAP ? G::L : 1;
   fragT zap[ZAP_H][ZAP_P];
-  // up1 A cache (CONV_UP1_CACHE): [32-B half][key 4 i + j (segment 1, 14 keys) / 2 i + k (segment 2, 8)]
-  constexpr bool UC = (CONV_UP1_CACHE && G::FUSED && G::S == 16 && sizeof(T) == 2 && G::STAGES == 3) ||
-                     (CONV_DOWN1_CACHE && G::PP);
+  // up1 A cache: [32-B half][key 4 i + j (segment 1, 14 keys) / 2 i + k (segment 2, 8)]
+  constexpr bool UC = G::FUSED && G::S == 16 && sizeof(T) == 2 && G::STAGES == 3;
   fragT uca[UC ? 2 : 1][UC ? 14 : 1];
 #pragma unroll
   for (int hh = 0; hh < (UC ? 2 : 1); ++hh)
@@ -1484,7 +1014,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     constexpr int SEG = SEGV == 4 ? 2 : SEGV;
     char* nbase = smem + nbuf * G::STAGE;
     if constexpr (G::W6) {
-      // up0 zero-skip, 6 fragments per wave (CONV_UP0_W6): wave (phase PAT, column half); step st = (k-group
+      // up0.fused, 6 fragments per wave: wave (phase PAT, column half); step st = (k-group
       // g, tap zs_tap(jj)); reads: the step's B fragment, then the positions first needed at this tap in the
       // first group of their A half; MFMAs of step st - 1: fragment f -> acc[f % 3][f / 3], A from zap.
       constexpr int PAT = decltype(pat_tag)::value;
@@ -1571,353 +1101,8 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         }
         __builtin_amdgcn_sched_barrier(0);
       });
-    } else if constexpr (G::ZS && CONV_UP0_ZS_CACHE) {
-      // up0 zero-skip, A fragments cached per position (zap[half][position]): step st = (k-group g, tap
-      // zs_tap(jj)); the reads of step st are B and the positions first needed at this tap in this half,
-      // the MFMAs of step st - 1 take their A operand from zap.  zap[h] is rewritten only by a later chunk's
-      // group of the same half, after every MFMA of this chunk's group has been issued (the carried last
-      // step at st = 0 reads the last group's half, never half 0).
-      constexpr int PAT = decltype(pat_tag)::value;
-      constexpr int NG = P3 ? 3 : ROWB / 32;
-      constexpr int NH = ROWB / 32;
-      constexpr int NT_ = SEG == 2 ? G::TAPS2 : TAPS;
-      constexpr int NS = NT_ * NG;
-      constexpr int NPER = NEXT == 3 ? G::PER2 : G::PER;
-      constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;
-      constexpr int PPS = (NPC + NS - 1) / NS;
-      constexpr bool M0 = (PAT & 1) == 0;
-      constexpr int HL = kg_a<P3>(NG - 1) >> 5;           // half of the last group (carried into st = 0)
-      static_assert(NS % 2 == 0 && HL != 0, "B double buffer alternates per step; carried half");
-      fragT am[SEG == 2 ? NH : 1];
-#pragma unroll
-      for (int st = 0; st < NS; ++st) {
-        const int g = st / NT_, jj = st % NT_, sb = st & 1, pb = sb ^ 1;
-        const int j = G::zs_tap(SEG, jj);
-        const int ah = kg_a<P3>(g) >> 5;
-        const bool fg = !P3 || g != 1;                    // the first group of its A half reads A
-        const int gp = st == 0 ? NG - 1 : (st - 1) / NT_;
-        const int jpp = G::zs_tap(SEG, (st == 0 ? NS - 1 : st - 1) % NT_);
-        const int ahp = kg_a<P3>(gp) >> 5;
-        int ao0, ao1, ao2, bo0, bo1;
-        if constexpr (SEG == 2) {
-          ao0 = aoff2[j][0]; ao1 = aoff2[j][1]; ao2 = aoff2[j][2]; bo0 = boff2[0]; bo1 = boff2[1];
-        } else {
-          ao0 = aoff[j][0]; ao1 = aoff[j][1]; ao2 = aoff[j][2]; bo0 = boff[0]; bo1 = boff[1];
-        }
-        const char* pa0 = base + (ao0 ^ kg_a<P3>(g));
-        const char* pa1 = base + (ao1 ^ kg_a<P3>(g));
-        const char* pa2 = base + (ao2 ^ kg_a<P3>(g));
-        const char* pb0 = base + ((bo0 + j * NT * ROWB) ^ kg_b<P3>(g));
-        const char* pb1 = base + ((bo1 + j * NT * ROWB) ^ kg_b<P3>(g));
-        auto rdA = [&](int i) { return fg && G::zs_ok(SEG, PAT, i, j) && G::zs_first(SEG, PAT, i, jj); };
-        auto body = [&](auto prev_tag) {
-          constexpr int PV = decltype(prev_tag)::value;   // 0: this segment's step st - 1; 1 / 2: segment 1's / 2's last
-          constexpr int SP = PV == 0 ? SEG : PV;            // segment of the MFMAs' step
-          auto okp = [&](int i) { return G::zs_ok(SP, PAT, i, PV == 0 ? jpp : SP == 2 ? G::TAPS2 - 1 : TAPS - 1); };
-          auto posp = [&](int i) { return G::zs_pos(SP, PAT, i, PV == 0 ? jpp : SP == 2 ? G::TAPS2 - 1 : TAPS - 1); };
-#define PETDIFF_ZMF(i, jn)                                                                                 \
-  if (okp(i)) {                                                                                            \
-    if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(zap[ahp][posp(i)], bv[pb][jn], acc[i][jn]);     \
-  }
-#define PETDIFF_ZRA(i, ptr) \
-  if (rdA(i)) { if constexpr (!(CONV_EXP_MODE & 64)) zap[ah][G::zs_pos(SEG, PAT, i, j)] = *reinterpret_cast<const fragT*>(ptr); }
-#define PETDIFF_ZRB(dst, ptr) \
-  if constexpr (!(CONV_EXP_MODE & 64)) dst = *reinterpret_cast<const fragT*>(ptr);
-          PETDIFF_ZMF(0, 0)
-          PETDIFF_ZRA(0, pa0)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_ZMF(1, 0)
-          PETDIFF_ZRB(bv[sb][0], pb0)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_ZMF(2, 0)
-          PETDIFF_ZRA(1, pa1)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_ZMF(0, 1)
-          PETDIFF_ZRA(2, pa2)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_ZMF(1, 1)
-          PETDIFF_ZRB(bv[sb][1], pb1)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_ZMF(2, 1)
-#undef PETDIFF_ZRB
-#undef PETDIFF_ZRA
-#undef PETDIFF_ZMF
-        };
-        if (st > 0) body(std::integral_constant<int, 0>{});
-        else if constexpr (SEG == 1 || SEGV == 4) body(std::integral_constant<int, 1>{});
-        else body(std::integral_constant<int, 2>{});
-        if constexpr (SEG == 2 && M0) {
-          if (st == 0) {
-#pragma unroll
-            for (int gg = 0; gg < NH; ++gg) am[gg] = *reinterpret_cast<const fragT*>(base + (amask ^ (gg << 5)));
-          }
-          if (st == 1) {
-#pragma unroll
-            for (int gg = 0; gg < NG; ++gg)
-#pragma unroll
-              for (int jn = 0; jn < 2; ++jn)
-                if constexpr (!(CONV_EXP_MODE & 2)) acc[0][jn] = mfma32(am[kg_a<P3>(gg) >> 5], epk[kg_b<P3>(gg) >> 5][jn], acc[0][jn]);
-            const int k2 = kc - dma.n1;
-            if (kc + 1 < NC) load_epk(k2 + 1);
-          }
-        }
-        if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
-#pragma unroll
-          for (int u = 0; u < PPS; ++u) {
-            const int k = st * PPS + u;
-            if (k < NPER) {
-              if constexpr (NEXT == 3) dma.piece2(nbase, k, nkc - dma.n1, lane);
-              else dma.piece1(nbase, k, nkc, lane);
-            } else if (NEXT == 2 && k < NPC) {
-              dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
-            }
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    } else if constexpr (G::ZS) {
-      // up0 zero-skip: step st = (k-group g, tap tap_of(jj)) in the tap-reuse path's order; the MFMAs
-      // of step st - 1 and the reads of step st, both over the (fragment, tap) pairs that read data.
-      // At st = 0 the MFMAs are the previous chunk's last step, of segment 1 when this is the first
-      // segment-2 chunk (SEGV == 4: peeled at compile time; a runtime choice there made the compiler
-      // shuffle the accumulators between two register assignments every chunk).
-      constexpr int PAT = decltype(pat_tag)::value;
-      constexpr int NG = P3 ? 3 : ROWB / 32;   // k-groups per chunk (paired bf16x3: 3)
-      constexpr int NH = ROWB / 32;             // 32-B halves of a row
-      constexpr int NT_ = SEG == 2 ? G::TAPS2 : TAPS;
-      constexpr int NS = NT_ * NG;
-      constexpr int NPER = NEXT == 3 ? G::PER2 : G::PER;
-      constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;
-      constexpr int PPS = (NPC + NS - 1) / NS;
-      constexpr bool M0 = (PAT & 1) == 0;                 // fragment 0 is coarse row 0 (edge correction)
-      static_assert(NS % 2 == 0, "fragment double buffer alternates per step");
-      fragT am[SEG == 2 ? NH : 1];
-      auto tap_of = [](int jj) { return SEG == 2 ? jj : (jj < 3 ? 2 * jj : 2 * (jj - 3) + 1); };
-      auto ok = [](int i, int j) { return SEG == 2 ? G::zs_valid2(PAT, i, j) : G::zs_valid1(PAT, i, j); };
-#pragma unroll
-      for (int st = 0; st < NS; ++st) {
-        const int g = st / NT_, jj = st % NT_, sb = st & 1, pb = sb ^ 1;
-        const int j = tap_of(jj);
-        const int jp = tap_of((st == 0 ? NS - 1 : st - 1) % NT_);
-        int ao0, ao1, ao2, bo0, bo1;
-        if constexpr (SEG == 2) {
-          ao0 = aoff2[j][0]; ao1 = aoff2[j][1]; ao2 = aoff2[j][2]; bo0 = boff2[0]; bo1 = boff2[1];
-        } else {
-          ao0 = aoff[j][0]; ao1 = aoff[j][1]; ao2 = aoff[j][2]; bo0 = boff[0]; bo1 = boff[1];
-        }
-        const char* pa0 = base + (ao0 ^ kg_a<P3>(g));
-        const char* pa1 = base + (ao1 ^ kg_a<P3>(g));
-        const char* pa2 = base + (ao2 ^ kg_a<P3>(g));
-        const char* pb0 = base + ((bo0 + j * NT * ROWB) ^ kg_b<P3>(g));
-        const char* pb1 = base + ((bo1 + j * NT * ROWB) ^ kg_b<P3>(g));
-        // the MFMAs of step st - 1 (fragment i, B half jn) and the reads of step st
-        auto body = [&](auto prev_tag) {
-          constexpr int PV = decltype(prev_tag)::value;   // 0: this segment's step st - 1; 1: segment 1's last; 2: segment 2's last
-          auto okp = [&](int i) {
-            return PV == 1 ? G::zs_valid1(PAT, i, TAPS - 1) : PV == 2 ? G::zs_valid2(PAT, i, G::TAPS2 - 1) : ok(i, jp);
-          };
-#define PETDIFF_ZMF(i, jn)                                                                                 \
-  if (okp(i)) {                                                                                            \
-    if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(av[pb][i], bv[pb][jn], acc[i][jn]);            \
-  }
-#define PETDIFF_ZRD(dst, ptr, valid) \
-  if (valid) { if constexpr (!(CONV_EXP_MODE & 64)) dst = *reinterpret_cast<const fragT*>(ptr); }
-          PETDIFF_ZMF(0, 0)
-          PETDIFF_ZRD(av[sb][0], pa0, ok(0, j))
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_CALL(PETDIFF_ZMF, PETDIFF_O1)
-          PETDIFF_ZRD(bv[sb][0], pb0, true)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_CALL(PETDIFF_ZMF, PETDIFF_O2)
-#if CONV_MFMA_ORDER
-          PETDIFF_ZRD(av[sb][1], pa1, ok(1, j))
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_CALL(PETDIFF_ZMF, PETDIFF_O3)
-          PETDIFF_ZRD(av[sb][2], pa2, ok(2, j))
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_CALL(PETDIFF_ZMF, PETDIFF_O4)
-          PETDIFF_ZRD(bv[sb][1], pb1, true)
-#else
-          PETDIFF_ZRD(bv[sb][1], pb1, true)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_CALL(PETDIFF_ZMF, PETDIFF_O3)
-          PETDIFF_ZRD(av[sb][1], pa1, ok(1, j))
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_CALL(PETDIFF_ZMF, PETDIFF_O4)
-          PETDIFF_ZRD(av[sb][2], pa2, ok(2, j))
-#endif
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_ZMF(2, 1)
-#undef PETDIFF_ZRD
-#undef PETDIFF_ZMF
-        };
-        if (st > 0) body(std::integral_constant<int, 0>{});
-        else if constexpr (SEG == 1 || SEGV == 4) body(std::integral_constant<int, 1>{});
-        else body(std::integral_constant<int, 2>{});
-        if constexpr (SEG == 2 && M0) {
-          // left-edge correction of the m = 0 rows, in the tap-reuse path's place: coarse row 0 read
-          // at step 0, multiplied after step 0's MFMAs (issued at step 1); then the next chunk's weights
-          if (st == 0) {
-#pragma unroll
-            for (int gg = 0; gg < NH; ++gg) am[gg] = *reinterpret_cast<const fragT*>(base + (amask ^ (gg << 5)));
-          }
-          if (st == 1) {
-#pragma unroll
-            for (int gg = 0; gg < NG; ++gg)
-#pragma unroll
-              for (int jn = 0; jn < 2; ++jn)
-                if constexpr (!(CONV_EXP_MODE & 2)) acc[0][jn] = mfma32(am[kg_a<P3>(gg) >> 5], epk[kg_b<P3>(gg) >> 5][jn], acc[0][jn]);
-            const int k2 = kc - dma.n1;
-            if (kc + 1 < NC) load_epk(k2 + 1);
-          }
-        }
-        if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
-#pragma unroll
-          for (int u = 0; u < PPS; ++u) {
-            const int k = st * PPS + u;
-            if (k < NPER) {
-              if constexpr (NEXT == 3) dma.piece2(nbase, k, nkc - dma.n1, lane);
-              else dma.piece1(nbase, k, nkc, lane);
-            } else if (NEXT == 2 && k < NPC) {
-              dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
-            }
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    } else if constexpr (REUSE) {
-      constexpr int NG = ROWB / 32;
-      constexpr int NT_ = SEG == 2 ? G::TAPS2 : TAPS;
-      constexpr int NS = NT_ * NG;
-      constexpr int D = SEG == 2 ? 1 : 2;                 // position step between fragments
-      constexpr int NPOS = NT_ + 2 * D;
-      constexpr int NPER = NEXT == 3 ? G::PER2 : G::PER;
-      constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;
-      constexpr int PPS = (NPC + NS - 1) / NS;
-      static_assert(NS % 2 == 0, "B double buffer alternates per step");
-      fragT AP[NG][NPOS];
-      fragT am[SEG == 2 ? NG : 1];
-      // edge correction folded into tap 0 (CONV_UP0_EDGE_TAP0): am is read by every wave (the zero
-      // row where no m = 0 rows), so the per-wave operand select never sees an undefined value
-      constexpr bool ETAP0 = CONV_UP0_EDGE_TAP0 && SEG == 2;
-      // LDS offset of relative position P (any (tap, fragment) pair that lands on it)
-      auto posoff = [&](int P) -> int {
-        if constexpr (SEG == 2) {
-          const int i = P < 2 ? P : 2;
-          return aoff2[P - i][i];
-        } else {
-          const int i = P / 2 < 2 ? P / 2 : 2;
-          return aoff[P - 2 * i][i];
-        }
-      };
-      // segment-1 tap order 0 2 4 1 3 5: consecutive taps of one parity share 2 of 3 positions
-      auto tap_of = [](int jj) { return SEG == 2 ? jj : (jj < 3 ? 2 * jj : 2 * (jj - 3) + 1); };
-#pragma unroll
-      for (int st = 0; st < NS; ++st) {
-        const int g = st / NT_, jj = st % NT_, sb = st & 1, pb = sb ^ 1;
-        const int j = tap_of(jj);
-        const bool full = SEG == 2 ? jj == 0 : (jj == 0 || jj == 3);
-        const int sp = st == 0 ? 0 : st - 1;
-        const int gp = sp / NT_, jp = tap_of(sp % NT_);
-        const char* pb0 = base + ((boff[0] + j * NT * ROWB) ^ (g << 5));
-        const char* pb1 = base + ((boff[1] + j * NT * ROWB) ^ (g << 5));
-        if constexpr (SEG == 2) {
-          pb0 = base + ((boff2[0] + j * NT * ROWB) ^ (g << 5));
-          pb1 = base + ((boff2[1] + j * NT * ROWB) ^ (g << 5));
-        }
-#define PETDIFF_RMF(i, jn)                                                                                 \
-  if constexpr (!(CONV_EXP_MODE & 2)) {                                                                    \
-    if (ETAP0 && (i) == 0 && st > 0 && jp == 0)                                                            \
-      acc[0][jn] = mfma32(has_m0 ? am[gp] : AP[gp][0], has_m0 ? epk[gp][jn] : bv[pb][jn], acc[0][jn]);    \
-    else                                                                                                   \
-      acc[i][jn] = mfma32(st == 0 ? cav[i] : AP[gp][jp + D * (i)], bv[pb][jn], acc[i][jn]);                \
-  }
-#define PETDIFF_RRD(dst, off) \
-  if constexpr (!(CONV_EXP_MODE & 64)) dst = *reinterpret_cast<const fragT*>(base + ((off) ^ (g << 5)));
-#define PETDIFF_BRD(dst, ptr) \
-  if constexpr (!(CONV_EXP_MODE & 64)) dst = *reinterpret_cast<const fragT*>(ptr);
-        if (full) {
-          PETDIFF_RMF(0, 0)
-          PETDIFF_RRD(AP[g][j], posoff(j))
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_RMF(0, 1)
-          PETDIFF_BRD(bv[sb][0], pb0)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_RMF(1, 0)
-          PETDIFF_BRD(bv[sb][1], pb1)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_RMF(1, 1)
-          PETDIFF_RRD(AP[g][j + D], posoff(j + D))
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_RMF(2, 0)
-          PETDIFF_RRD(AP[g][j + 2 * D], posoff(j + 2 * D))
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_RMF(2, 1)
-        } else {
-          PETDIFF_RMF(0, 0)
-          PETDIFF_BRD(bv[sb][0], pb0)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_RMF(0, 1)
-          PETDIFF_BRD(bv[sb][1], pb1)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_RMF(1, 0)
-          PETDIFF_RRD(AP[g][j + 2 * D], posoff(j + 2 * D))
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_RMF(1, 1)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_RMF(2, 0)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_RMF(2, 1)
-        }
-#undef PETDIFF_BRD
-#undef PETDIFF_RRD
-#undef PETDIFF_RMF
-        if constexpr (ETAP0) {
-          if (st == 0) {
-#pragma unroll
-            for (int gg = 0; gg < NG; ++gg) am[gg] = *reinterpret_cast<const fragT*>(base + (amask ^ (gg << 5)));
-          }
-          // the last k-group's tap-0 MFMAs (step (NG - 1) NT_, issued at the step after it) use epk
-          if (st == (NG - 1) * NT_ + 1 && has_m0) {
-            const int k2 = kc - dma.n1;
-            if (kc + 1 < NC) load_epk(k2 + 1);
-          }
-        } else if constexpr (SEG == 2) {
-          if (st == 0 && has_m0) {
-#pragma unroll
-            for (int gg = 0; gg < NG; ++gg) am[gg] = *reinterpret_cast<const fragT*>(base + (amask ^ (gg << 5)));
-          }
-          if (st == 1 && has_m0) {
-#pragma unroll
-            for (int gg = 0; gg < NG; ++gg)
-#pragma unroll
-              for (int jn = 0; jn < 2; ++jn)
-                if constexpr (!(CONV_EXP_MODE & 2)) acc[0][jn] = mfma32(am[gg], epk[gg][jn], acc[0][jn]);
-            const int k2 = kc - dma.n1;
-            if (kc + 1 < NC) load_epk(k2 + 1);
-          }
-        }
-        if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
-#pragma unroll
-          for (int u = 0; u < PPS; ++u) {
-            const int k = st * PPS + u;
-            if (k < NPER) {
-              if constexpr (NEXT == 3) dma.piece2(nbase, k, nkc - dma.n1, lane);
-              else dma.piece1(nbase, k, nkc, lane);
-            } else if (NEXT == 2 && k < NPC) {
-              dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
-            }
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      {
-        constexpr int jl = SEG == 2 ? NT_ - 1 : TAPS - 1;   // the last step's tap (order ends on 5 / 3)
-#pragma unroll
-        for (int i = 0; i < 3; ++i) cav[i] = AP[NG - 1][jl + D * i];
-      }
-    } else if constexpr (G::PW6) {
-      // position-major, 6 fragments per wave (CONV_PM_W6): step st = (tap j, k-group g) as the other PM
+    } else if constexpr (G::PM) {
+      // position-major, 6 fragments per wave: step st = (tap j, k-group g) as the generic
       // paths; reads: the step's B fragment, then the set's positions first needed at tap j (first group of
       // their half); MFMAs of step st - 1: fragment f -> acc[f % 3][f / 3], A from zap.
       constexpr int NG = P3 ? 3 : ROWB / 32;
@@ -1973,139 +1158,8 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         }
         __builtin_amdgcn_sched_barrier(0);
       });
-    } else if constexpr (G::PM && CONV_PM_CACHE) {
-      // position-major, A fragments cached per input position (zap[half][position], CONV_PM_CACHE): step
-      // st = (tap j, k-group g); the reads of step st are B and the positions that this set first needs at
-      // tap j (in the first group of their half), the MFMAs of step st - 1 take A from zap.  A position is
-      // rewritten only by the next chunk's first use of its half, after this chunk's last MFMA on it.
-      constexpr int NG = P3 ? 3 : ROWB / 32;
-      constexpr int NS = TAPS * NG;
-      constexpr int NPER = G::PER;
-      constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;
-      constexpr int PPS = (NPC + NS - 1) / NS;
-      static_assert(NS % 2 == 0 && (kg_a<P3>(NG - 1) >> 5) != 0, "B double buffer alternates per step; carried half");
-      {
-        constexpr int PAT = decltype(pat_tag)::value;
-#pragma unroll
-        for (int st = 0; st < NS; ++st) {
-          const int j = st / NG, g = st % NG, sb = st & 1, pb = sb ^ 1;
-          const int jp = st == 0 ? TAPS - 1 : (st - 1) / NG;
-          const int gp = st == 0 ? NG - 1 : (st - 1) % NG;
-          const int ah = kg_a<P3>(g) >> 5, ahp = kg_a<P3>(gp) >> 5;
-          const bool fg = !P3 || g != 1;                  // the first group of its A half reads A
-          const char* pa0 = base + (aoff[j][0] ^ kg_a<P3>(g));
-          const char* pa1 = base + (aoff[j][1] ^ kg_a<P3>(g));
-          const char* pa2 = base + (aoff[j][2] ^ kg_a<P3>(g));
-          const char* pb0 = base + ((boff[0] + j * NT * ROWB) ^ kg_b<P3>(g));
-          const char* pb1 = base + ((boff[1] + j * NT * ROWB) ^ kg_b<P3>(g));
-#define PETDIFF_CMF(i, jn)                                                                                  \
-  if (G::pm_valid(PAT, i, jp)) {                                                                            \
-    if constexpr (!(CONV_EXP_MODE & 2))                                                                     \
-      acc[i][jn] = mfma32(zap[ahp][G::pm_pos(PAT, i) + jp - PADL], bv[pb][jn], acc[i][jn]);                  \
-  }
-#define PETDIFF_CRA(i, ptr)                                                                                 \
-  if (fg && G::pm_valid(PAT, i, j) && G::pm_first(PAT, i, j)) {                                             \
-    if constexpr (!(CONV_EXP_MODE & 64)) zap[ah][G::pm_pos(PAT, i) + j - PADL] = *reinterpret_cast<const fragT*>(ptr); \
-  }
-#define PETDIFF_CRB(dst, ptr) \
-  if constexpr (!(CONV_EXP_MODE & 64)) dst = *reinterpret_cast<const fragT*>(ptr);
-          PETDIFF_CMF(0, 0)
-          PETDIFF_CRA(0, pa0)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_CMF(1, 0)
-          PETDIFF_CRB(bv[sb][0], pb0)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_CMF(2, 0)
-          PETDIFF_CRA(1, pa1)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_CMF(0, 1)
-          PETDIFF_CRA(2, pa2)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_CMF(1, 1)
-          PETDIFF_CRB(bv[sb][1], pb1)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_CMF(2, 1)
-#undef PETDIFF_CRB
-#undef PETDIFF_CRA
-#undef PETDIFF_CMF
-          if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
-#pragma unroll
-            for (int u = 0; u < PPS; ++u) {
-              const int k = st * PPS + u;
-              if (k < NPER) dma.piece1(nbase, k, nkc, lane);
-              else if (NEXT == 2 && k < NPC) dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
-            }
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-    } else if constexpr (G::PM) {
-      // position-major down3: step st = (tap j, k-group g); the MFMAs of step st - 1 and the reads
-      // of step st, both over this wave's valid fragments only (pm_valid folds after unrolling)
-      constexpr int NG = P3 ? 3 : ROWB / 32;   // k-groups per chunk (paired bf16x3: 3)
-      constexpr int NS = TAPS * NG;
-      constexpr int NPER = G::PER;
-      constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;
-      constexpr int PPS = (NPC + NS - 1) / NS;
-      static_assert(NS % 2 == 0, "fragment double buffer alternates per step");
-      {
-        constexpr int PAT = decltype(pat_tag)::value;
-#pragma unroll
-        for (int st = 0; st < NS; ++st) {
-          const int j = st / NG, g = st % NG, sb = st & 1, pb = sb ^ 1;
-          const int jp = st == 0 ? TAPS - 1 : (st - 1) / NG;   // st = 0: the previous chunk's last step
-          const char* pa0 = base + (aoff[j][0] ^ kg_a<P3>(g));
-          const char* pa1 = base + (aoff[j][1] ^ kg_a<P3>(g));
-          const char* pa2 = base + (aoff[j][2] ^ kg_a<P3>(g));
-          const char* pb0 = base + ((boff[0] + j * NT * ROWB) ^ kg_b<P3>(g));
-          const char* pb1 = base + ((boff[1] + j * NT * ROWB) ^ kg_b<P3>(g));
-#define PETDIFF_PMF(i, jn)                                                                                 \
-  if (G::pm_valid(PAT, i, jp)) {                                                                           \
-    if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(av[pb][i], bv[pb][jn], acc[i][jn]);            \
-  }
-#define PETDIFF_PRD(dst, ptr, ok) \
-  if (ok) { if constexpr (!(CONV_EXP_MODE & 64)) dst = *reinterpret_cast<const fragT*>(ptr); }
-          PETDIFF_PMF(0, 0)
-          PETDIFF_PRD(av[sb][0], pa0, G::pm_valid(PAT, 0, j))
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_CALL(PETDIFF_PMF, PETDIFF_O1)
-          PETDIFF_PRD(bv[sb][0], pb0, true)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_CALL(PETDIFF_PMF, PETDIFF_O2)
-#if CONV_MFMA_ORDER
-          PETDIFF_PRD(av[sb][1], pa1, G::pm_valid(PAT, 1, j))
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_CALL(PETDIFF_PMF, PETDIFF_O3)
-          PETDIFF_PRD(av[sb][2], pa2, G::pm_valid(PAT, 2, j))
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_CALL(PETDIFF_PMF, PETDIFF_O4)
-          PETDIFF_PRD(bv[sb][1], pb1, true)
-#else
-          PETDIFF_PRD(bv[sb][1], pb1, true)
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_CALL(PETDIFF_PMF, PETDIFF_O3)
-          PETDIFF_PRD(av[sb][1], pa1, G::pm_valid(PAT, 1, j))
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_CALL(PETDIFF_PMF, PETDIFF_O4)
-          PETDIFF_PRD(av[sb][2], pa2, G::pm_valid(PAT, 2, j))
-#endif
-          __builtin_amdgcn_sched_barrier(0);
-          PETDIFF_PMF(2, 1)
-#undef PETDIFF_PRD
-#undef PETDIFF_PMF
-          if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
-#pragma unroll
-            for (int u = 0; u < PPS; ++u) {
-              const int k = st * PPS + u;
-              if (k < NPER) dma.piece1(nbase, k, nkc, lane);
-              else if (NEXT == 2 && k < NPC) dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
-            }
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
     } else if constexpr (UC) {
-      // up1 with cached A fragments (CONV_UP1_CACHE): step st = (tap j, k-group g) as the generic path;
+      // up1 with cached A fragments: step st = (tap j, k-group g) as the generic path;
       // reads: B and the keys first needed at tap j (first group of their half); MFMAs of step st - 1 take
       // A from uca[half][key].  At st = 0 they are the previous chunk's last step, of segment 1 for the
       // first segment-2 chunk (SEGV == 4, peeled).
@@ -2116,7 +1170,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       constexpr int NPER = NEXT == 3 ? G::PER2 : G::PER;
       constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;
       constexpr int PPS = (NPC + NS - 1) / NS;
-      constexpr int KS = (SEG == 2 || G::PP) ? 2 : 4;     // key step between fragments
+      constexpr int KS = SEG == 2 ? 2 : 4;                // key step between fragments
       static_assert(NS % 2 == 0 && (kg_a<P3>(NG - 1) >> 5) != 0, "B double buffer alternates per step; carried half");
       fragT am[SEG == 2 ? NH : 1];
       static_for<0, NS>([&](auto st_tag) {
@@ -2126,7 +1180,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         constexpr int ah = kg_a<P3>(g) >> 5, ahp = kg_a<P3>(gp) >> 5;
         constexpr bool fg = !P3 || g != 1;
         // previous step's segment key step and tap
-        constexpr int KSP = st > 0 ? KS : G::PP ? 2 : (SEG == 1 || SEGV == 4) ? 4 : 2;
+        constexpr int KSP = st > 0 ? KS : (SEG == 1 || SEGV == 4) ? 4 : 2;
         constexpr int JP = st > 0 ? (st - 1) / NG : (SEG == 1 || SEGV == 4) ? TAPS - 1 : G::TAPS2 - 1;
         int ao0, ao1, ao2, bo0, bo1;
         if constexpr (SEG == 2) {
@@ -2210,7 +1264,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       for (int st = 0; st < NS; ++st) {
         const int j = st / NG, g = st % NG, sb = st & 1;
         // interleave one fragment read per MFMA gap, in the order the next step's
-        // MFMAs consume them (A0 B0 B1 A1 A2); each (MFMA, read) pair is pinned
+        // MFMAs consume them (A0 B0 A1 A2 B1); each (MFMA, read) pair is pinned
         int ao0, ao1, ao2, bo0, bo1;
         if constexpr (SEG == 2) {
           ao0 = aoff2[j][0]; ao1 = aoff2[j][1]; ao2 = aoff2[j][2]; bo0 = boff2[0]; bo1 = boff2[1];
@@ -2231,27 +1285,17 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         PETDIFF_MF(0, 0)
         PETDIFF_RD(av[sb][0], pa0)
         __builtin_amdgcn_sched_barrier(0);
-        PETDIFF_CALL(PETDIFF_MF, PETDIFF_O1)
+        PETDIFF_MF(1, 0)
         PETDIFF_RD(bv[sb][0], pb0)
         __builtin_amdgcn_sched_barrier(0);
-        PETDIFF_CALL(PETDIFF_MF, PETDIFF_O2)
-#if CONV_MFMA_ORDER
+        PETDIFF_MF(2, 0)
         PETDIFF_RD(av[sb][1], pa1)
         __builtin_amdgcn_sched_barrier(0);
-        PETDIFF_CALL(PETDIFF_MF, PETDIFF_O3)
+        PETDIFF_MF(0, 1)
         PETDIFF_RD(av[sb][2], pa2)
         __builtin_amdgcn_sched_barrier(0);
-        PETDIFF_CALL(PETDIFF_MF, PETDIFF_O4)
+        PETDIFF_MF(1, 1)
         PETDIFF_RD(bv[sb][1], pb1)
-#else
-        PETDIFF_RD(bv[sb][1], pb1)
-        __builtin_amdgcn_sched_barrier(0);
-        PETDIFF_CALL(PETDIFF_MF, PETDIFF_O3)
-        PETDIFF_RD(av[sb][1], pa1)
-        __builtin_amdgcn_sched_barrier(0);
-        PETDIFF_CALL(PETDIFF_MF, PETDIFF_O4)
-        PETDIFF_RD(av[sb][2], pa2)
-#endif
         __builtin_amdgcn_sched_barrier(0);
         PETDIFF_MF(2, 1)
 #undef PETDIFF_RD
@@ -2464,25 +1508,12 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       __syncthreads();
     } else {
       dma.all(smem, 0, 0, lane);
-      // CONV_MAPS_LATE: the map prefetches go out after B0 instead of right behind chunk 0.  At
-      // kernel start all 256 workgroups' bursts share the fabric, so the final level's 50 KB of map
-      // rows per workgroup would delay every chunk 0 (prologue 4.6 us on up2 against 2.8 on up0);
-      // issued after B0 they stream during the K loop and still retire at B1.
-      constexpr bool FINMID = CONV_FIN_MAPS_MID && G::FIN_MAPS && !CONV_MAPS_LATE;
-      if constexpr (!CONV_MAPS_LATE) {
-        prefetch_maps();
-        if constexpr (!FINMID) prefetch_fin_maps();
-      }
+      prefetch_maps();
+      prefetch_fin_maps();
       // B0: chunk 0 landed; the maps (issued after it, NMAPW per wave) may still be in flight --
       // B1 below retires them together with chunk 1, long before the epilogue reads them
       static_assert(NMAPW + 1 + 2 * G::PER < 64 && NMAPW + 1 + 2 * G::PER2 < 64, "vmcnt range");
-      if constexpr (CONV_MAPS_LATE) {
-        ring_barrier<0>();
-        prefetch_maps();
-        prefetch_fin_maps();
-      } else if constexpr (FINMID) {
-        ring_barrier<NMAPW - G::FMAP_FULL>();          // the final maps go out later (FIN_MAPS_KM)
-      } else if (map_extra) {
+      if (map_extra) {
         ring_barrier<NMAPW + 1>();
       } else {
         ring_barrier<NMAPW>();
@@ -2497,19 +1528,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         int buf = 1, kc = 1;
         for (; kc + 2 < n1; ++kc) {
           compute(smem + buf * G::STAGE, Yes{}, kc + 2, buf == 0 ? 2 : buf - 1, Seg1{}, 0, pat_tag);
-          if constexpr (FINMID) {
-            static_assert(!FINMID || FIN_MAPS_KM >= 1, "maps after the first loop chunk");
-            // host guarantees n1 >= FIN_MAPS_KM + 4 on the final level (n1 = 8 bf16 / fp16, 24 bf16x3)
-            if (kc == FIN_MAPS_KM) prefetch_fin_maps();
-            if (kc == FIN_MAPS_KM || kc == FIN_MAPS_KM + 1) {
-              if (map_extra) ring_barrier<G::PER + G::FMAP_FULL + 1>();
-              else ring_barrier<G::PER + G::FMAP_FULL>();
-            } else {
-              ring_barrier<G::PER>();
-            }
-          } else {
-            ring_barrier<G::PER>();
-          }
+          ring_barrier<G::PER>();
           buf = buf == 2 ? 0 : buf + 1;
         }
         for (; kc < n1; ++kc) {                              // the next chunks are segment 2
@@ -2517,7 +1536,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
           ring_barrier<G::PER2>();
           buf = buf == 2 ? 0 : buf + 1;
         }
-        if constexpr (G::ZS || UC) {   // the first segment-2 chunk, peeled (n2 >= 3: up0 32 / 96, up1 16 / 32)
+        if constexpr (G::W6 || UC) {   // the first segment-2 chunk, peeled (n2 >= 3: up0 32 / 96, up1 16 / 32)
           compute(smem + buf * G::STAGE, Seg2Next{}, kc + 2, buf == 0 ? 2 : buf - 1, Seg2First{}, kc, pat_tag);
           ring_barrier<G::PER2>();
           buf = buf == 2 ? 0 : buf + 1;
@@ -2533,21 +1552,10 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         buf = buf == 2 ? 0 : buf + 1;
         compute(smem + buf * G::STAGE, No{}, 0, 0, Seg2{}, kc + 1, pat_tag);
         ring_barrier<0>();
-        if constexpr (G::ZS) {   // the last chunk's last step (composite tap 3) over this set's valid fragments
+        if constexpr (G::W6) {   // the last chunk's last step (composite tap 3) over this set's valid fragments
           constexpr int PAT = decltype(pat_tag)::value;
           constexpr int HL = kg_a<P3>((P3 ? 3 : ROWB / 32) - 1) >> 5;
-#pragma unroll
-          for (int i = 0; i < 3; ++i)
-            if (G::zs_valid2(PAT, i, G::TAPS2 - 1))
-#pragma unroll
-              for (int jn = 0; jn < 2; ++jn)
-                if constexpr (!(CONV_EXP_MODE & 2) && !G::W6) {
-                  if constexpr (CONV_UP0_ZS_CACHE)
-                    acc[i][jn] = mfma32(zap[HL][G::zs_pos(2, PAT, i, G::TAPS2 - 1)], bv[1][jn], acc[i][jn]);
-                  else
-                    acc[i][jn] = mfma32(av[1][i], bv[1][jn], acc[i][jn]);
-                }
-          if constexpr (G::W6 && !(CONV_EXP_MODE & 2)) {
+          if constexpr (!(CONV_EXP_MODE & 2)) {
 #pragma unroll
             for (int f = 0; f < 6; ++f)
               if (G::w6_ok(2, PAT, f, G::TAPS2 - 1))
@@ -2555,15 +1563,10 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
           }
         }
       };
-      // up0 zero-skip: each wave's fragment set gets its own main loop (no per-step branch)
+      // up0: each wave's output phase gets its own main loop (no per-step branch)
       if constexpr (G::W6) {
         if (w6e == 0) fused_loop(P0{});
         else fused_loop(std::integral_constant<int, 1>{});
-      } else if constexpr (G::ZS) {
-        if (wmu == 0) fused_loop(P0{});
-        else if (wmu == 1) fused_loop(std::integral_constant<int, 1>{});
-        else if (wmu == 2) fused_loop(std::integral_constant<int, 2>{});
-        else fused_loop(std::integral_constant<int, 3>{});
       } else {
         fused_loop(P0{});
       }
@@ -2587,54 +1590,10 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     // Loader waves: chunk c lands in stage c % 3; barrier B(c+1) closes the MFMA waves'
     // work on chunk c, after which stage c % 3 takes chunk c + 3.
     if (loader) {
-#if CONV_LDR_EARLY
-      // all three stages are free at kernel start: chunks 1 and 2 go out right behind chunk 0,
-      // and B0 waits (counted vmcnt) for chunk 0's pieces only
-      static_assert(2 * G::PER < 64, "vmcnt range");
       dma.all(smem, 0, 0, lane);
-      if (NC > 1) dma.all(smem, 1, 1, lane);
-      if (NC > 2) dma.all(smem, 2, 2, lane);
-      if (NC > 2) ring_barrier<2 * G::PER>();              // B0: chunk 0 landed
-      else if (NC > 1) ring_barrier<G::PER>();
-      else ring_barrier<0>();
-#else
-      if constexpr (SEAM == 2) {
-        // seam consumer: chunk 0's weights first, then wait for the producers of this tile's samples
-#pragma unroll
-        for (int k = G::APT; k < G::PER; ++k) dma.piece(smem, k, 0, lane);
-        const int g = m_tile, want = sa.prod_n * min(sa.per_grp / sa.prod_n, sa.n_prod_m - g * (sa.per_grp / sa.prod_n));
-#ifndef CONV_SEAM_ONE_FENCE
-#define CONV_SEAM_ONE_FENCE 1   // 1: loader wave 0 polls and acquires for the CU, a workgroup barrier releases the
-                                //    other waves (the MFMA waves join it before B0); 0: every loader wave polls and
-                                //    acquires (4 L1 invalidates per CU: about 9 us of prologue, scripts/micro/seam_micro)
-#endif
-        if (!CONV_SEAM_ONE_FENCE || w == 0) {
-          if (lane == 0) {
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            while (__hip_atomic_load(sa.grp + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-              __builtin_amdgcn_s_sleep(2);
-              if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {   // 20 ms: give up, do not hang
-                __hip_atomic_fetch_add(sa.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-              }
-            }
-#if CONV_EXP_MODE & 128
-            if (w == 0) reinterpret_cast<unsigned long long*>(a.fin.x_all)[12288 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-#endif
-          }
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // this CU's L1 (one invalidate covers every wave)
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // ... and it has completed
-        }
-        if (CONV_SEAM_ONE_FENCE) __builtin_amdgcn_s_barrier();  // the seam barrier (MFMA waves: before B0)
-#pragma unroll
-        for (int k = 0; k < G::APT; ++k) dma.piece(smem, k, 0, lane);
-      } else {
-        dma.all(smem, 0, 0, lane);
-      }
       ring_barrier<0>();                                   // B0: chunk 0 landed
       if (NC > 1) dma.all(smem, 1, 1, lane);
       if (NC > 2) dma.all(smem, 2, 2, lane);
-#endif
       for (int kc = 0; kc < NC; ++kc) {
         if (kc + 2 < NC) ring_barrier<G::PER>();           // chunk kc+1 landed, kc+2 in flight
         else ring_barrier<0>();
@@ -2642,25 +1601,19 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       }
     } else {
       prefetch_maps();
-      if constexpr (SEAM == 2) {
-        if (CONV_SEAM_ONE_FENCE) __builtin_amdgcn_s_barrier();   // the seam barrier: loader wave 0 has acquired
-      }
       ring_barrier<0>();                                   // B0 (maps landed too)
 #if CONV_EXP_MODE & 128
       st_c0 = __builtin_amdgcn_s_memtime();
       st_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
       auto mainloop = [&](auto pat_tag) {
-#if CONV_MFMA_PRIO
-        __builtin_amdgcn_s_setprio(CONV_MFMA_PRIO);   // MFMA waves win issue over the loader wave on their SIMD
-#endif
         int buf = 0;
         for (int kc = 0; kc < NC; ++kc) {
           compute(smem + buf * G::STAGE, No{}, 0, 0, Seg1{}, 0, pat_tag);
           ring_barrier<0>();                               // B(kc+1): own LDS reads done
           buf = buf == 2 ? 0 : buf + 1;
         }
-        if constexpr (G::PW6) {   // the last step (tap TAPS - 1) of this set's valid fragments
+        if constexpr (G::PM) {   // the last step (tap TAPS - 1) of this set's valid fragments
           constexpr int SET = decltype(pat_tag)::value;
           constexpr int HL = kg_a<P3>((P3 ? 3 : ROWB / 32) - 1) >> 5;
 #pragma unroll
@@ -2668,34 +1621,12 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
             if (G::pw6_valid(SET, f, TAPS - 1))
               if constexpr (!(CONV_EXP_MODE & 2))
                 acc[f % 3][f / 3] = mfma32(zap[HL][G::pw6_pos(SET, f) + TAPS - 1 - PADL], bv[1][0], acc[f % 3][f / 3]);
-        } else if constexpr (G::PM) {   // the last step (tap TAPS - 1) of this wave's valid fragments
-          constexpr int PAT = decltype(pat_tag)::value;
-          constexpr int HL = kg_a<P3>((P3 ? 3 : ROWB / 32) - 1) >> 5;
-#pragma unroll
-          for (int i = 0; i < 3; ++i)
-            if (G::pm_valid(PAT, i, TAPS - 1))
-#pragma unroll
-              for (int jn = 0; jn < 2; ++jn)
-                if constexpr (!(CONV_EXP_MODE & 2)) {
-                  if constexpr (CONV_PM_CACHE)
-                    acc[i][jn] = mfma32(zap[HL][G::pm_pos(PAT, i) + TAPS - 1 - PADL], bv[1][jn], acc[i][jn]);
-                  else
-                    acc[i][jn] = mfma32(av[1][i], bv[1][jn], acc[i][jn]);
-                }
         }
       };
       // position-major: each fragment set gets its own main loop (no per-chunk branch)
-      if constexpr (G::PW6) {
+      if constexpr (G::PM) {
         if (pw6set == 0) mainloop(P0{});
         else mainloop(std::integral_constant<int, 1>{});
-      } else if constexpr (G::PM && G::NPAT == 4) {
-        if (pm_pat == 0) mainloop(P0{});
-        else if (pm_pat == 1) mainloop(std::integral_constant<int, 1>{});
-        else if (pm_pat == 2) mainloop(std::integral_constant<int, 2>{});
-        else mainloop(std::integral_constant<int, 3>{});
-      } else if constexpr (G::PM) {
-        if (pm_pat != 0) mainloop(std::integral_constant<int, 1>{});
-        else mainloop(P0{});
       } else {
         mainloop(P0{});
       }
@@ -2753,13 +1684,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   }
   }
   if (loader) return;   // s_barrier waits only for the waves still running
-  if constexpr (REUSE) {   // the last chunk's last step: carried A operands, B in bv[1] (NS even)
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int jn = 0; jn < 2; ++jn)
-        if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(cav[i], bv[1][jn], acc[i][jn]);
-  } else if constexpr (G::PM || G::ZS) {
+  if constexpr (G::PM || G::W6) {
     // flushed at the end of the position-major / zero-skip main loop
   } else if constexpr (UC) {   // the last chunk's last step: composite tap 3 of the last group's half
     constexpr int HL = kg_a<P3>((P3 ? 3 : ROWB / 32) - 1) >> 5;
@@ -2767,7 +1692,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int jn = 0; jn < 2; ++jn)
-        if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(uca[HL][2 * i + (G::PP ? TAPS : G::TAPS2) - 1], bv[1][jn], acc[i][jn]);
+        if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(uca[HL][2 * i + G::TAPS2 - 1], bv[1][jn], acc[i][jn]);
   } else {
     mfma_bf16(1);   // the last chunk's last step (NS even)
   }
@@ -2803,22 +1728,6 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     // The tile interleaves row pairs ([r/2][c][2]): an accumulator's consecutive rows
     // (rg, rg+1) go out as one ds_write_b64 and a row pair comes back as 4 ds_read_b128.
     float* ct = reinterpret_cast<float*>(smem);
-    if constexpr (G::PP) {
-      // pair-position-major fragments: accumulator rows rg < 8 are position 2F of sample s, rg + 8
-      // the same sample at 2F + 1 -- written as the sample-major row pair, so the epilogue below
-      // (pooled pairs = two positions of one sample) is the sample-major one
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int jn = 0; jn < 2; ++jn)
-#pragma unroll
-          for (int rg = 0; rg < 8; ++rg) {
-            const int r = wm * 96 + i * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * h;   // bit 4 clear
-            const int rs = (r & 15) * L + 2 * (r >> 5);                           // (s, 2F): even
-            *reinterpret_cast<float2*>(ct + (rs >> 1) * G::CT_LD + (wn * 64 + jn * 32 + lr) * 2) =
-                make_float2(acc[i][jn][rg], acc[i][jn][rg + 8]);
-          }
-    } else
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -2828,9 +1737,9 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
           // W6: accumulator (i, jn) is fragment f = 3 jn + i (coarse row f of phase w6e), columns 32 w6h + lr
           // PW6: fragment f = 3 jn + i is position pw6_pos(pw6set, f) of sample half pw6_sh, at its PM tile row
           const int r = (G::W6    ? w6e * G::PHROWS + (3 * jn + i) * G::S
-                         : G::PW6 ? G::pm_row(G::pw6_pos(pw6set, 3 * jn + i), G::pw6_sh(pw6set) * 32)
-                                  : G::frag_row(wmu, i)) + (rg & 3) + 8 * (rg >> 2) + 4 * h;   // even
-          *reinterpret_cast<float2*>(ct + (r >> 1) * G::CT_LD + (G::W6 || G::PW6 ? w6h * 32 + lr : wn * 64 + jn * 32 + lr) * 2) =
+                         : G::PM ? G::pm_row(G::pw6_pos(pw6set, 3 * jn + i), G::pw6_sh(pw6set) * 32)
+                                  : G::frag_row(wm, i)) + (rg & 3) + 8 * (rg >> 2) + 4 * h;   // even
+          *reinterpret_cast<float2*>(ct + (r >> 1) * G::CT_LD + (G::W6 || G::PM ? w6h * 32 + lr : wn * 64 + jn * 32 + lr) * 2) =
               make_float2(acc[i][jn][rg], acc[i][jn][rg + 1]);
         }
     __syncthreads();
@@ -2936,24 +1845,6 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     if (mode == 1) epi_rows(std::integral_constant<int, 1>{});
     else if (mode == 2) epi_rows(std::integral_constant<int, 2>{});
     else epi_rows(std::integral_constant<int, 0>{});
-    if constexpr (SEAM != 0) {
-      // every storing wave drains its write-through stores; then one lane signals for the workgroup
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        if constexpr (SEAM == 1) {
-          __hip_atomic_fetch_add(sa.grp + m_tile / (sa.per_grp / sa.prod_n), 1, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-          // the last consumer resets the counters for the next launch (every producer has signalled by
-          // then: every consumer waited for its producers)
-          if (__hip_atomic_fetch_add(sa.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == sa.n_cons - 1) {
-            for (int k = 0; k < sa.n_grp; ++k) __hip_atomic_store(sa.grp + k, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(sa.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
-      }
-    }
 #if CONV_EXP_MODE & 128
     if (tid == 0) reinterpret_cast<unsigned long long*>(a.fin.x_all)[4096 + 2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
@@ -3024,13 +1915,8 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       if constexpr ((FIN_EXP & 4) != 0) { xst[r * 2] = xst[r * 2 + 1] = fin[r * G::FIN_LD]; goto fin_rows_done; }
       const float* mp = a.tmap ? a.tmap + ((size_t)t * L + l) * cout : nullptr;
       const float* cp = a.cmap ? a.cmap + ((size_t)tac * L + l) * cout : nullptr;
-      f32x4 o4 = {0.f, 0.f, 0.f, 0.f}, o4b = {0.f, 0.f, 0.f, 0.f};
-      // FIN_SCALAR_W: with 4 outputs the final kernel [128][4] is read wave-uniformly through the
-      // scalar cache (constant address space) instead of 128 LDS reads per row.  FIN_SPLIT: odd
-      // channels accumulate separately (dependent FMA chains of 64 instead of 128).
-      typedef const __attribute__((address_space(4))) f32x4 cf32x4;
-      cf32x4* cw = (cf32x4*)(uintptr_t)f.wf;
-      auto dot = [&](const float* mq, const float* cq, auto scalar_w) {
+      f32x4 o4 = {0.f, 0.f, 0.f, 0.f};
+      auto dot = [&](const float* mq, const float* cq) {
 #pragma unroll 4
         for (int n = 0; n < 128; n += 4) {
           f32x4 hv = *reinterpret_cast<const f32x4*>(fin + r * G::FIN_LD + n);
@@ -3039,22 +1925,17 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const float hq = fmaxf(hv[q], 0.f);
-            f32x4 wq;
-            if constexpr (decltype(scalar_w)::value) wq = cw[n + q];
-            else wq = *reinterpret_cast<const f32x4*>(wfl + (n + q) * 4);
-            f32x4& acc = (FIN_SPLIT && (q & 1)) ? o4b : o4;
-            acc[0] = fmaf(hq, wq[0], acc[0]);
-            acc[1] = fmaf(hq, wq[1], acc[1]);
-            acc[2] = fmaf(hq, wq[2], acc[2]);
-            acc[3] = fmaf(hq, wq[3], acc[3]);
+            const f32x4 wq = *reinterpret_cast<const f32x4*>(wfl + (n + q) * 4);
+            o4[0] = fmaf(hq, wq[0], o4[0]);
+            o4[1] = fmaf(hq, wq[1], o4[1]);
+            o4[2] = fmaf(hq, wq[2], o4[2]);
+            o4[3] = fmaf(hq, wq[3], o4[3]);
           }
         }
       };
       const bool fin_lds = G::FIN_MAPS && fin_fast;   // the same map rows, prefetched into LDS
       const float* lm = reinterpret_cast<const float*>(smem + G::FMAP_OFF) + l * G::FIN_LD;
-      if (FIN_SCALAR_W && n_out == 4) dot(fin_lds ? lm : mp, fin_lds ? lm + G::FMAP_STRIDE * 4 : cp, std::true_type{});
-      else dot(fin_lds ? lm : mp, fin_lds ? lm + G::FMAP_STRIDE * 4 : cp, std::false_type{});
-      if (FIN_SPLIT) o4 += o4b;
+      dot(fin_lds ? lm : mp, fin_lds ? lm + G::FMAP_STRIDE * 4 : cp);
       float o[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) o[q] = o4[q] + bfin[q];
@@ -3095,47 +1976,8 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
 #pragma unroll
         for (int k = 0; k < 6; ++k) reinterpret_cast<f32x4*>(mp)[tid + kThreads * k] = mv[k];
       }
-      // fused down1 of the next step (16-bit networks: bf16, fp16, bf16x3; PETDIFF_FUSE_DOWN1=1): level-1
-      // map rows loaded now, written to LDS after down0.  A tile with more than one condition (per-sample
-      // tac; rare: TAC-major batches change condition at tile boundaries) reads them from L2 per sample
-      using DL = D1L<XS>;
-      constexpr bool D1 = sizeof(T) == 2 && G::FIN_MAPS;
-      const bool fuse_d1 = D1 && f.d1_w != nullptr;
-      const bool d1_mixed = fuse_d1 && !fast;
-      static_assert(!D1 || DL::M + DL::MAPB <= G::MT * G::FIN_LD * 4, "fused down1 tiles fit the dead C tile");
-      static_assert(!D1 || (G::SMEM == 162560 && DL::slot_off(DL::NS_HI - 1) + DL::UNIT <= G::SMEM &&
-                                        (DL::NS_HI >= DL::NS || DL::UNIT <= DL::A)), "fused down1 B ring fits the LDS");
-      static_assert(!D1 || G::MT / L == 4, "fused down1: 4 samples per tile");
-      f32x4 m1v[6];
-      if (fuse_d1) {
-        if (!d1_mixed) {
-          const int tac_d1 = nd.tac ? nd.tac[m0] : 0;
-          const f32x4* tm1 = reinterpret_cast<const f32x4*>(f.d1_tmap + (size_t)nd.t_uniform * 24 * 256);
-          const f32x4* cm1 = reinterpret_cast<const f32x4*>(f.d1_cmap + (size_t)tac_d1 * 24 * 256);
-#pragma unroll
-          for (int k = 0; k < 6; ++k) m1v[k] = tm1[tid + kThreads * k] + cm1[tid + kThreads * k];
-        }
-        // zero row + the rows of absent samples (their outputs are not stored; keep them finite)
-        for (int q = tid; q < (DL::Rows + 1 - nb_next * 24) * (DL::Ldb / 16); q += kThreads)
-          *reinterpret_cast<uint4*>(smem + DL::A + nb_next * 24 * DL::Ldb + q * 16) = make_uint4(0, 0, 0, 0);
-      }
       __syncthreads();
-      if constexpr (!(FIN_EXP & 1)) down0_positions<T, XS>(nd, xst, mp, fast, m0, nb_next, wr, n0_next, tid >> 4, kThreads / 16,
-                                                           fuse_d1 ? smem + DL::A : nullptr);
-      if constexpr (D1) {
-        if (fuse_d1) {
-          if (!d1_mixed) {
-#pragma unroll
-            for (int k = 0; k < 6; ++k) reinterpret_cast<f32x4*>(smem + DL::M)[tid + kThreads * k] = m1v[k];
-          }
-          __syncthreads();                             // p0 rows (and the level-1 maps) in LDS; down0 done
-#if CONV_EXP_MODE & 128
-          if (tid == 0) reinterpret_cast<unsigned long long*>(a.fin.x_all)[6144 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-#endif
-          if (d1_mixed) fused_down1_lds<T, XS, true>(f, smem, m0, nb_next, wv, lane, nd.t_uniform, nd.tac, B);
-          else fused_down1_lds<T, XS, false>(f, smem, m0, nb_next, wv, lane, nd.t_uniform, nd.tac, B);
-        }
-      }
+      if constexpr (!(FIN_EXP & 1)) down0_positions<T, XS>(nd, xst, mp, fast, m0, nb_next, wr, n0_next, tid >> 4, kThreads / 16);
 #if CONV_EXP_MODE & 128
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -3148,19 +1990,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
 template <typename T, int KIND, int XS = 0>
 __global__ __launch_bounds__(conv_max_threads<KIND>(), 1) void conv_kernel(ConvArgs<T> a) {
   __shared__ __attribute__((aligned(16))) char smem[ConvGeom<T, KIND>::SMEM];
-  conv_body<T, KIND, XS, 0>(a, smem, blockIdx.x, SeamArgs{});
-}
-
-// down2 -> down3 in one launch (SeamArgs): blocks [0, n_prod) = down2 tiles, the rest down3 tiles
-template <typename T, int XS>
-__global__ __launch_bounds__(2 * kThreads, 1) void seam23_kernel(ConvArgs<T> a2, ConvArgs<T> a3, SeamArgs sa) {
-  constexpr int S2 = ConvGeom<T, LK_DOWN2>::SMEM, S3 = ConvGeom<T, LK_DOWN3>::SMEM;
-  static_assert(ConvGeom<T, LK_DOWN2>::NTH == 2 * kThreads && ConvGeom<T, LK_DOWN3>::NTH == 2 * kThreads,
-                "both layers run the 8-wave loader shape");
-  __shared__ __attribute__((aligned(16))) char smem[S2 > S3 ? S2 : S3];
-  const int b = blockIdx.x;
-  if (b < sa.n_prod) conv_body<T, LK_DOWN2, XS, 1>(a2, smem, b, sa);
-  else conv_body<T, LK_DOWN3, XS, 2>(a3, smem, b - sa.n_prod, sa);
+  conv_body<T, KIND, XS>(a, smem, blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -3393,15 +2223,13 @@ __global__ void posterior_stats_kernel(const float* x0, const int* tac, int B, i
   }
 }
 
-// {seed, sample_offset + start_k} pairs of the counter-based noise stream (FinalArgs::rng), written
-// on the stream from kernel arguments: no host buffer has to outlive the call (graph replays
-// read the pairs from device memory, so a cached graph serves every seed)
-__global__ void set_rng_kernel(unsigned long long* dst, unsigned long long seed, unsigned long long off0,
-                               unsigned long long off1, int parts) {
-  const int k = threadIdx.x;
-  if (k < parts) {
-    dst[2 * k] = seed;
-    dst[2 * k + 1] = k == 0 ? off0 : off1;
+// {seed, sample_offset} of the counter-based noise stream (FinalArgs::rng), written on the stream from
+// kernel arguments: no host buffer has to outlive the call (graph replays read the pair from device
+// memory, so a cached graph serves every seed)
+__global__ void set_rng_kernel(unsigned long long* dst, unsigned long long seed, unsigned long long off) {
+  if (threadIdx.x == 0) {
+    dst[0] = seed;
+    dst[1] = off;
   }
 }
 
@@ -3433,12 +2261,6 @@ static hipError_t launch_one(const ConvArgs<T>& a, hipStream_t s) {
   const int nM = (a.B + G::S - 1) / G::S;
   const int total = nM * (a.cout / G::NT);
   hipLaunchKernelGGL((conv_kernel<T, KIND, XS>), dim3(total), dim3(G::NTH), 0, s, a);
-  return hipGetLastError();
-}
-
-template <typename T, int XS>
-static hipError_t launch_seam23_xs(const ConvArgs<T>& a2, const ConvArgs<T>& a3, const SeamArgs& sa, hipStream_t s) {
-  hipLaunchKernelGGL((seam23_kernel<T, XS>), dim3(sa.n_prod + sa.n_cons), dim3(2 * kThreads), 0, s, a2, a3, sa);
   return hipGetLastError();
 }
 
@@ -3490,44 +2312,11 @@ hipError_t launch_down0(const Down0Args& a, hipStream_t s, bool x3) {
   return hipGetLastError();
 }
 
-// down2 + down3 in one launch (PETDIFF_SEAM23); seam_state: int [n_grp + 2] zeroed once at allocation
-template <typename T>
-hipError_t launch_seam23(const ConvArgs<T>& a2, const ConvArgs<T>& a3, int* seam_state, hipStream_t s, bool x3) {
-  if constexpr (sizeof(T) != 2) {
-    return hipErrorInvalidValue;
-  } else {
-    using G2 = ConvGeom<T, LK_DOWN2>;
-    using G3 = ConvGeom<T, LK_DOWN3>;
-    if (a2.B <= 0) return hipSuccess;
-    static_assert(G3::S % G2::S == 0, "a down3 sample block is whole down2 M tiles");
-    SeamArgs sa;
-    const int n2m = (a2.B + G2::S - 1) / G2::S, n3m = (a3.B + G3::S - 1) / G3::S;
-    sa.prod_n = a2.cout / G2::NT;
-    sa.n_prod = n2m * sa.prod_n;
-    sa.n_cons = n3m * (a3.cout / G3::NT);
-    sa.n_grp = n3m;
-    sa.per_grp = (G3::S / G2::S) * sa.prod_n;
-    sa.n_prod_m = n2m;
-    sa.grp = seam_state;
-    sa.done = seam_state + n3m;
-    sa.err = seam_state + n3m + 1;
-    if (a2.cout % G2::NT || a3.cout % G3::NT || a2.c1 % G2::KC || a3.c1 % G3::KC) return hipErrorInvalidValue;
-    if (x3) {
-      if constexpr (std::is_same<T, bf16>::value) return launch_seam23_xs<T, 1>(a2, a3, sa, s);
-      return hipErrorInvalidValue;
-    }
-    return launch_seam23_xs<T, 0>(a2, a3, sa, s);
-  }
-}
-template hipError_t launch_seam23<bf16>(const ConvArgs<bf16>&, const ConvArgs<bf16>&, int*, hipStream_t, bool);
-template hipError_t launch_seam23<f16>(const ConvArgs<f16>&, const ConvArgs<f16>&, int*, hipStream_t, bool);
-template hipError_t launch_seam23<float>(const ConvArgs<float>&, const ConvArgs<float>&, int*, hipStream_t, bool);
 template hipError_t launch_conv<bf16>(int, const ConvArgs<bf16>&, hipStream_t, bool);
 template hipError_t launch_conv<f16>(int, const ConvArgs<f16>&, hipStream_t, bool);
 template hipError_t launch_conv<float>(int, const ConvArgs<float>&, hipStream_t, bool);
-hipError_t launch_set_rng(unsigned long long* dst, unsigned long long seed, unsigned long long off0,
-                          unsigned long long off1, int parts, hipStream_t s) {
-  hipLaunchKernelGGL(set_rng_kernel, dim3(1), dim3(64), 0, s, dst, seed, off0, off1, parts);
+hipError_t launch_set_rng(unsigned long long* dst, unsigned long long seed, unsigned long long off, hipStream_t s) {
+  hipLaunchKernelGGL(set_rng_kernel, dim3(1), dim3(64), 0, s, dst, seed, off);
   return hipGetLastError();
 }
 

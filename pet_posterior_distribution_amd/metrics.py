@@ -172,11 +172,15 @@ def _z_scale(x):
 
 def _rhat_basic(x):
     """Gelman-Rubin R-hat of (chains, draws, ...): sqrt((B / W + n - 1) / n) with B = n var(chain means),
-    W = mean within-chain variance (ddof = 1 both)."""
+    W = mean within-chain variance (ddof = 1 both).
+    W = 0 (constant chains) gives NaN without a floating-point warning; rhat() masks those parameters."""
     n = x.shape[1]
     b = n * np.var(x.mean(axis=1), axis=0, ddof=1)
     w = np.mean(np.var(x, axis=1, ddof=1), axis=0)
-    return np.sqrt((b / w + n - 1) / n)
+    ok = w > 0
+    out = np.full(np.shape(w), np.nan)
+    out[ok] = np.sqrt((b[ok] / w[ok] + n - 1) / n)
+    return out
 
 
 def rhat(draws):

@@ -1,0 +1,60 @@
+#!/bin/bash
+# Round-4 GPU check of the working tree.  Stages (STAGES, default "bitwise tests bench"):
+#   bitwise  scripts/lib_bitwise.py dumps of every ALT build (scripts/micro/alt/<name>.so) and of this
+#            build, compared array by array (bf16 / fp16 / bf16x3 forwards + 20-step loops)
+#   tests    the GPU test suite;  smoke  __graft_entry__.smoke()
+#   bench    the driver's bench command (1 GPU) and a rocprofv3 kernel-stats pass
+#   ab       REPS interleaved bench pairs: this build vs each ALT (BENCH_EXTRA: more bench flags)
+# Usage: ALTS="pre_prune.so" STAGES="bitwise tests" bash scripts/gpu_r4.sh TAG
+set -o pipefail
+TAG=${1:-r4}
+STAGES=${STAGES:-"bitwise tests bench"}
+REPS=${REPS:-2}
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+has() { [[ " $STAGES " == *" $1 "* ]]; }
+if has bitwise; then
+  timeout -k 10 300 python scripts/lib_bitwise.py dump $OUT/cur.npz > $OUT/bitwise.txt 2>&1 || { echo "dump failed"; exit 1; }
+  for alt in $ALTS; do
+    PETDIFF_LIB=$GRAFT_REPO_ROOT/scripts/micro/alt/$alt timeout -k 10 300 python scripts/lib_bitwise.py dump $OUT/${alt%.so}.npz >> $OUT/bitwise.txt 2>&1 || { echo "dump $alt failed"; exit 1; }
+    echo "== $alt vs this build" >> $OUT/bitwise.txt
+    python scripts/lib_bitwise.py compare $OUT/${alt%.so}.npz $OUT/cur.npz >> $OUT/bitwise.txt 2>&1
+  done
+  grep -E "==|ALL|differ" $OUT/bitwise.txt
+fi
+if has tests; then
+  timeout -k 10 900 python -u -m pytest tests -q -m gpu -p no:cacheprovider --timeout 200 --timeout-method thread \
+    ${PYTEST_ARGS} > $OUT/pytest.log 2>&1
+  rc=$?
+  echo "pytest exit $rc" >> $OUT/pytest.log
+  tail -4 $OUT/pytest.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest died ($rc)"; exit $rc; fi
+fi
+if has smoke; then
+  timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; exit 1; }
+  tail -1 $OUT/smoke.log
+fi
+if has bench; then
+  timeout -k 10 500 python bench.py --gpus 1 --steps 20 --warmup 5 ${BENCH_EXTRA} > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail $OUT/bench.err; exit 1; }
+  head -c 400 $OUT/bench.json; echo
+  timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 2 --no-cpu-baseline --no-extras ${BENCH_EXTRA} > $OUT/bench_prof.log 2>&1 || { echo "rocprof failed"; exit 1; }
+  timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof_x3 -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 2 --no-cpu-baseline --no-extras --dtype bf16x3 > $OUT/bench_prof_x3.log 2>&1 || { echo "rocprof x3 failed"; exit 1; }
+fi
+if has ab; then
+  for rep in $(seq 1 $REPS); do
+    for d in bfloat16 bf16x3; do
+      timeout -k 10 300 python bench.py --steps 3 --no-cpu-baseline --no-extras --dtype $d > $OUT/ab_cur_${d}_$rep.json 2>/dev/null || exit 1
+      for alt in $ALTS; do
+        PETDIFF_LIB=$GRAFT_REPO_ROOT/scripts/micro/alt/$alt timeout -k 10 300 python bench.py --steps 3 --no-cpu-baseline --no-extras --dtype $d > $OUT/ab_${alt%.so}_${d}_$rep.json 2>/dev/null || exit 1
+      done
+    done
+  done
+  python - <<PY
+import json, glob
+for f in sorted(glob.glob('$OUT/ab_*.json')):
+    d = json.load(open(f)); print(f.split('/')[-1], round(d['value'], 1), {k: round(v, 2) for k, v in d.get('layer_us', {}).items() if v})
+PY
+fi
+echo EXIT 0

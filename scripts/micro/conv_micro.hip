@@ -25,7 +25,6 @@ __global__ void fill_f32(float* p, size_t n, unsigned seed) {
   }
 }
 
-static bool g_with_d1 = false;
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
 template <int KIND>
@@ -93,21 +92,6 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
   a.fin.next.x = xn; a.fin.next.w0 = w0; a.fin.next.cmap = m0c; a.fin.next.tmap = m0t;
   a.fin.next.tac = nullptr; a.fin.next.tvec = nullptr; a.fin.next.t_uniform = G::EPI == EPI_FINAL ? 499 : -1;
   a.fin.next.s0 = s0n; a.fin.next.p0 = p0n; a.fin.next.B = B;
-  // the final level's fused next-step down1 (argv[3] = "d1"): packed weights [4 n-tiles][4 chunks][6][64][64 B],
-  // level-1 maps and the s1 / p1 outputs
-  bf16 *d1w = nullptr, *d1s1 = nullptr, *d1p1 = nullptr;
-  float *d1t = nullptr, *d1c = nullptr;
-  if (g_with_d1 && G::EPI == EPI_FINAL) {
-    CK(hipMalloc(&d1w, 4 * 4 * 6 * 64 * 64));
-    CK(hipMalloc(&d1t, (size_t)1000 * 24 * 256 * 4));
-    CK(hipMalloc(&d1c, 24 * 256 * 4));
-    CK(hipMalloc(&d1s1, (size_t)B * 24 * 256 * 2));
-    CK(hipMalloc(&d1p1, (size_t)B * 12 * 256 * 2));
-    fill_bf16<<<1024, 256>>>(d1w, 4 * 4 * 6 * 64 * 32, 15);
-    fill_f32<<<1024, 256>>>(d1t, (size_t)1000 * 24 * 256, 16);
-    fill_f32<<<64, 256>>>(d1c, 24 * 256, 17);
-    a.fin.d1_w = d1w; a.fin.d1_tmap = d1t; a.fin.d1_cmap = d1c; a.fin.d1_s1 = d1s1; a.fin.d1_p1 = d1p1;
-  }
   unsigned long long* dbg;
   // stamps [0, 8192 + 4 * grid) plus, on the final level, the keep_all_xt rows it writes through x_all
   const size_t dbg_bytes = 6 * 4096 * 8 + (size_t)B * 96 * 4;
@@ -165,24 +149,6 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
            mx(st), med(pro), mx(pro), med(lp), mx(lp), med(epi), mx(epi), (tmax - tmin) * 0.01);
     printf("   epilogue us: acc->LDS+barrier %.2f | read/add/store issue %.2f | store drain %.2f\n", med(ea), med(eb),
            med(ec));
-    if (G::EPI == EPI_FINAL && g_with_d1) {   // the fused down1 starts at stamp 6144 + b (after down0)
-      std::vector<unsigned long long> d6(nb);
-      CK(hipMemcpy(d6.data(), dbg + 6144, nb * 8, hipMemcpyDeviceToHost));
-      std::vector<double> dz, dd;
-      for (int b = 0; b < nb; ++b) {
-        dz.push_back((d6[b] - e2[2 * b + 1]) * 0.01);
-        dd.push_back((t4[4 * b + 3] - d6[b]) * 0.01);
-      }
-      std::vector<unsigned long long> d7(nb);
-      CK(hipMemcpy(d7.data(), dbg + 7168, nb * 8, hipMemcpyDeviceToHost));
-      std::vector<double> dk, de;
-      for (int b = 0; b < nb; ++b) {
-        dk.push_back(d7[b] ? (d7[b] - d6[b]) * 0.01 : 0.0);
-        de.push_back(d7[b] ? (t4[4 * b + 3] - d7[b]) * 0.01 : 0.0);
-      }
-      printf("   final epilogue us: staging %.2f | row loop %.2f | down0 + maps %.2f | fused down1 %.2f (max %.2f)"
-             " = K loop %.2f + epilogue and drain %.2f\n", med(ea), med(eb), med(dz), med(dd), mx(dd), med(dk), med(de));
-    }
     printf("   loop cycles median %.0f (%.1f per MFMA), clock median %.3f GHz [%.3f..%.3f]\n", cyc[nb / 2],
            cyc[nb / 2] / nmfma, clk[nb / 2], clk[0], clk[nb - 1]);
   }
@@ -194,15 +160,13 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
   hipFree(s1); if (s2) hipFree(s2); hipFree(w); hipFree(out); hipFree(pool); hipFree(cmap); hipFree(tmap);
   hipFree(bias); hipFree(wf); hipFree(bfv); hipFree(xt); hipFree(xn); hipFree(tab); hipFree(rng); hipFree(dbg);
   hipFree(ep); hipFree(w0); hipFree(m0c); hipFree(m0t); hipFree(s0n); hipFree(p0n);
-  if (d1w) { hipFree(d1w); hipFree(d1t); hipFree(d1c); hipFree(d1s1); hipFree(d1p1); }
 }
 
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 1024;
   const int it = 200;
   const char* only = argc > 2 ? argv[2] : "";
-  g_with_d1 = argc > 3 && std::string(argv[3]) == "d1";
-  if (std::string(only) == "u2") {   // the final level alone (with argv[3] = d1: its fused down1)
+  if (std::string(only) == "u2") {   // the final level alone
     run<LK_UP2_F>("up2.fused", B, 128, 256, 128, it);
     return 0;
   }

@@ -442,6 +442,10 @@ def test_bench_pmc_fields_per_dtype_and_build(monkeypatch):
         pmc = bench.load_pmc(True, dt)
         assert pmc['stale'] and pmc['mfma_busy'] is None and pmc['traffic'] is None
         assert bench.pmc_fields(pmc, 70e-6)['mfma_util'] is None
+        # a build without a recognisable code-object hash never matches, not even a stamp of None
+        monkeypatch.setattr(_lib, 'kernel_code_hash', lambda *a, **k: None)
+        pmc = bench.load_pmc(True, dt)
+        assert pmc['stale'] and pmc['traffic'] is None
 
 
 def test_reference_prior_fixture():

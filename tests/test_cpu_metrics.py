@@ -96,3 +96,20 @@ def test_rhat_rank_normalised_split():
     rep = convergence_report(t, n_roi=4)
     assert rep['flag'] and rep['rhat_max'] == np.nanmax(rhat(t))
     assert not convergence_report(np.concatenate([x[:, :, :4], x[:, :, :4]], 2), n_roi=4)['flag']
+
+
+def test_rhat_constant_draws_nan_without_warnings():
+    """A parameter whose draws are constant (a chain that never moved, e.g. an un-tuned MH element) gets
+    NaN, and the within-chain variance W = 0 raises no floating-point warning (the GPU test log carried
+    divide / invalid warnings from it in round 3)."""
+    import warnings
+    from pet_posterior_distribution_amd.metrics import rhat
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((4, 200, 3))
+    x[..., 1] = 2.5                                      # constant everywhere
+    x[:, :, 2] = np.arange(4)[:, None]                   # constant within each chain, different chains
+    with warnings.catch_warnings():
+        warnings.simplefilter('error')
+        r = rhat(x)
+    assert np.isfinite(r[0]) and np.isnan(r[1])
+    assert np.isnan(r[2]) or r[2] > 1.02                 # W ~ 0 up to rounding: never reads as converged

@@ -79,6 +79,12 @@ def conds():
 
 
 @pytest.fixture(scope='module')
+def trained():
+    from tests.helpers import quick_trained_weights
+    return quick_trained_weights()
+
+
+@pytest.fixture(scope='module')
 def m32():
     return make_model('float32')
 
@@ -198,16 +204,22 @@ def test_loop_injected_noise_f32(m32, conds, sub):
         assert rel(f(o, axis=0), f(ref, axis=0)) < 1e-4
 
 
-def test_loop_full_1000_steps_f32(m32, conds):
-    """Full T=1000 reverse process (the metric's path) at small B vs the oracle."""
+def test_loop_full_1000_steps_f32(trained):
+    """Full T=1000 reverse process (the metric's path) at small B vs the fp64 oracle, 1e-4, with the
+    briefly trained eps-predictor (tests.helpers.quick_trained_weights: no identity shortcut, so the
+    bound covers the whole U-Net's contribution, as test_loop_full_1000_steps_bf16x3)."""
+    from tests.test_gpu_parity16 import make
+    W, cond = trained
+    m = make(W, 'float32')
     rng = np.random.default_rng(7)
     B = 2
     x = rng.standard_normal((B, 48, 2)).astype(np.float32)
     idx = R.loop_indices(1000)
     z = rng.standard_normal((len(idx), B, 48, 2)).astype(np.float32)
-    out = m32.ddpm_loop(x, conds[:1], z=z)
-    ref = R.ddpm_loop(m32.network.weights, S, x, conds[:1], z, idx, dt=np.float64)
+    out = m.ddpm_loop(x, cond[None], z=z)
+    ref = R.ddpm_loop(W, S, x, cond[None], z, idx, dt=np.float64)
     assert rel(out, ref) < 1e-4
+    m.close()
 
 
 def test_config1_posterior_mean_sd_f32(m32, conds):
@@ -359,85 +371,33 @@ def test_fused_next_step_down0_bitwise(conds, dtype, monkeypatch):
     fused.close()
 
 
-@pytest.mark.parametrize('dtype', ['bfloat16', 'float16', 'bf16x3'])
-def test_fused_next_step_down1_bitwise(conds, dtype, monkeypatch):
-    """PETDIFF_FUSE_DOWN1=1 also runs step i+1's down1 (Conv1D 128 -> 256 + MaxPool) inside step i's
-    final epilogue, on the tile's own p0 rows (the 16-bit networks: bf16, fp16 and bf16x3's 12 hi/lo
-    chunks; off by default since round 3 -- a wash against the standalone launch -- PETDIFF_FUSE_DOWN1=1).  Same operands and fp32
-    MFMA accumulation order as the standalone conv_kernel<down1>: bit-identical samples, ragged batch (an
-    incomplete last tile), graph and eager, one condition (the LDS map path) and conditions interleaved
-    per sample (tiles with several conditions: per-sample level-1 maps)."""
-    rng = np.random.default_rng(25)
-    B = 37
-    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
-    table = np.stack([conds[0], conds[1], conds[0] * 0.9 + 0.05])
-    tac = rng.integers(0, 3, B).astype(np.int32)
-    monkeypatch.setenv('PETDIFF_FUSE_DOWN1', '0')
-    plain = make_model(dtype)
-    plain._ensure_handle()
-    monkeypatch.setenv('PETDIFF_FUSE_DOWN1', '1')
-    fused = make_model(dtype)
-    fused._ensure_handle()
-    for kw in ({'tac': tac}, {}):
-        cset = table if kw else conds[:1]
-        for g in (True, False):
-            a = plain.ddpm_loop(x, cset, num_timesteps=25, seed=4, use_graph=g, **kw)
-            b = fused.ddpm_loop(x, cset, num_timesteps=25, seed=4, use_graph=g, **kw)
-            torch.testing.assert_close(a, b, rtol=0, atol=0)
-    plain.close()
-    fused.close()
-
-
-@pytest.mark.parametrize('dtype', ['bfloat16', 'float16', 'bf16x3'])
-def test_seam23_bitwise(conds, dtype, monkeypatch):
-    """PETDIFF_SEAM23=1 runs down2 and down3 in one launch (blocks [0, n) = down2 tiles; a down3 tile waits on
-    a per-sample-block counter of the down2 tiles that feed it, then acquires).  Same per-tile arithmetic as
-    the two launches: bit-identical forward (ragged batches: a last sample block with one down2 M tile) and
-    graph loops, repeated launches (the counters reset themselves)."""
-    rng = np.random.default_rng(27)
-    monkeypatch.setenv('PETDIFF_SEAM23', '0')
-    plain = make_model(dtype)
-    plain._ensure_handle()
-    monkeypatch.setenv('PETDIFF_SEAM23', '1')
-    seam = make_model(dtype)
-    seam._ensure_handle()
-    table = np.stack([conds[0], conds[1]])
-    for B in (5, 37, 96, 1024):
-        x = rng.standard_normal((B, 48, 2)).astype(np.float32)
-        t = rng.integers(0, 1000, B).astype(np.int32)
-        cond = table[rng.integers(0, 2, B)]
-        torch.testing.assert_close(plain.call({'x': x, 'time': t, 'condition': cond}),
-                                   seam.call({'x': x, 'time': t, 'condition': cond}), rtol=0, atol=0)
-    x = rng.standard_normal((256, 48, 2)).astype(np.float32)
-    for _ in range(2):
-        a = plain.ddpm_loop(x, conds[:1], num_timesteps=30, seed=4)
-        b = seam.ddpm_loop(x, conds[:1], num_timesteps=30, seed=4)
-        torch.testing.assert_close(a, b, rtol=0, atol=0)
-    plain.close()
-    seam.close()
-
-
-def test_split_streams_bitwise(conds, monkeypatch):
-    """PETDIFF_SPLIT=2 runs the batch as two sample ranges, each its own graph on its own
-    stream: identical samples to the single-graph run (counter-based noise, per-sample math)."""
+@pytest.mark.parametrize('fuse_down0', ['1', '0'])
+def test_graph_segments_bitwise(conds, fuse_down0, monkeypatch):
+    """PETDIFF_GRAPH_SEG=7 captures the 30-step loop as 5 graph segments (the last one ragged: 2 steps)
+    launched back to back; the fused next-step down0 crosses every segment boundary (step i's epilogue
+    writes step i + 1's s0 / p0).  Bit-identical to the single-graph loop and to eager launches, for one
+    condition and for conditions interleaved per sample, with the fused down0 on and off."""
     rng = np.random.default_rng(24)
     B = 200
     x = rng.standard_normal((B, 48, 2)).astype(np.float32)
     table = np.stack([conds[0], conds[1]])
     tac = rng.integers(0, 2, B).astype(np.int32)
-    monkeypatch.setenv('PETDIFF_SPLIT', '1')
+    monkeypatch.setenv('PETDIFF_FUSE_DOWN0', fuse_down0)
+    monkeypatch.setenv('PETDIFF_GRAPH_SEG', '0')
     one = make_model('bfloat16')
-    one._ensure_handle()
-    monkeypatch.setenv('PETDIFF_SPLIT', '2')
-    two = make_model('bfloat16')
-    two._ensure_handle()
+    one._ensure_handle()                       # the switches are read when the handle is created
+    monkeypatch.setenv('PETDIFF_GRAPH_SEG', '7')
+    seg = make_model('bfloat16')
+    seg._ensure_handle()
     for kw in ({'tac': tac}, {}):
         cset = table if kw else conds[:1]
         a = one.ddpm_loop(x, cset, num_timesteps=30, seed=8, sample_offset=5, **kw)
-        b = two.ddpm_loop(x, cset, num_timesteps=30, seed=8, sample_offset=5, **kw)
+        b = seg.ddpm_loop(x, cset, num_timesteps=30, seed=8, sample_offset=5, **kw)
+        c = seg.ddpm_loop(x, cset, num_timesteps=30, seed=8, sample_offset=5, use_graph=False, **kw)
         torch.testing.assert_close(a, b, rtol=0, atol=0)
+        torch.testing.assert_close(a, c, rtol=0, atol=0)
     one.close()
-    two.close()
+    seg.close()
 
 
 @pytest.mark.parametrize('dtype', ['bfloat16', 'float16'])
