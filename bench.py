@@ -58,6 +58,48 @@ EXEC_MFMA_FLOP_PER_SAMPLE_STEP_FUSED = int(
     2 * 24 * 6 * 128 * 256 + 2 * 12 * 6 * 256 * 512 * 63 / 72 + 2 * 6 * 6 * 512 * 1024 * 54 / 72 +
     sum(2 * L * 6 * cs * co + 2 * L * 4 * cb * co + 2 * 2 * cb * co
         for L, cs, cb, co in ((12, 512, 1024, 512), (24, 256, 512, 256), (48, 128, 256, 128))))
+# Per-launch work of the step's kernels (SURVEY App. A MACs per sample-step; x2 = FLOP).  Each entry:
+# (timing key, kernel, algorithmic MAC per sample, MFMA MAC the 16-bit kernel executes per sample).
+# Executed: the label / time channels live in the hoisted maps, the 1x1 residual is folded into the
+# centre tap, and the position-major down2 / down3 and up0 skip the (position, tap) products that read
+# SAME padding (63 / 72, 54 / 72; up0: 63 of 72 skip-half and 20 of 24 composite products per phase).
+# up2.fused also runs the final 1x1 conv, p_sample and the NEXT step's down0 (VALU, not in the MFMA count).
+STEP_KERNELS = (
+    ('down1', 'conv_kernel<down1> (L=24, 178->256 k6+res, MaxPool)', 24 * 7 * 178 * 256, 24 * 6 * 128 * 256),
+    ('down2', 'conv_kernel<down2> (L=12, 306->512 k6+res, MaxPool)', 12 * 7 * 306 * 512, 12 * 6 * 256 * 512 * 63 // 72),
+    ('down3', 'conv_kernel<down3> (L=6, 562->1024 k6+res)', 6 * 7 * 562 * 1024, 6 * 6 * 512 * 1024 * 54 // 72),
+    ('up0.block', 'conv_kernel<up0 fused> (UpSampling1D + k2 1074->512 + ConvBlock 1024->512 k6+res, L=12)',
+     12 * 2 * 1074 * 512 + 12 * 7 * 1024 * 512, UP0_FUSED_EXEC_FLOP_PER_SAMPLE // 2),
+    ('up1.block', 'conv_kernel<up1 fused> (UpSampling1D + k2 562->256 + ConvBlock 512->256 k6+res, L=24)',
+     24 * 2 * 562 * 256 + 24 * 7 * 512 * 256, 24 * 6 * 256 * 256 + 24 * 4 * 512 * 256 + 2 * 512 * 256),
+    ('up2.block', 'conv_kernel<up2 fused> (UpSampling1D + k2 306->128 + ConvBlock 256->128 k6+res, L=48) + final '
+                  '1x1 128->4 + p_sample + next-step down0 (52->128 k6+res)',
+     48 * 2 * 306 * 128 + 48 * 7 * 256 * 128 + 48 * 128 * 4 + 48 * 7 * 52 * 128,
+     48 * 6 * 128 * 128 + 48 * 4 * 256 * 128 + 2 * 256 * 128),
+)
+
+
+def step_kernel_bytes(key, dtype):
+    """Algorithmic HBM bytes per sample of a step kernel: its input activation rows read once, its
+    output rows written once (16-bit: 2 B per value; bf16x3: [hi | lo] rows, 4 B), x_t / x_{t-1} fp32 for
+    the final level.  The packed weights (read once per launch) are added by weight_bytes."""
+    e = 4 if dtype in ('bf16x3', 'float32') else 2
+    acts = {'down1': 24 * 128 + 24 * 256 + 12 * 256, 'down2': 12 * 256 + 12 * 512 + 6 * 512,
+            'down3': 6 * 512 + 6 * 1024, 'up0.block': 12 * 512 + 6 * 1024 + 12 * 512,
+            'up1.block': 24 * 256 + 12 * 512 + 24 * 256,
+            'up2.block': 48 * 128 + 24 * 256 + 48 * 128 + 24 * 128}[key]   # up2: + next s0 / p0
+    return acts * e + (2 * 96 * 4 if key == 'up2.block' else 0)
+
+
+def weight_bytes(key, dtype):
+    """Packed weight bytes of a step kernel (x channels only; the fused levels' composite taps)."""
+    e = 4 if dtype in ('bf16x3', 'float32') else 2
+    w = {'down1': 6 * 128 * 256, 'down2': 6 * 256 * 512, 'down3': 6 * 512 * 1024,
+         'up0.block': 6 * 512 * 512 + 8 * 1024 * 512, 'up1.block': 6 * 256 * 256 + 8 * 512 * 256,
+         'up2.block': 6 * 128 * 128 + 8 * 256 * 128}[key]
+    return w * e
+
+
 # training step (SURVEY 8(f) row 4): forward + data grad + weight grad of every layer, incl. the
 # per-sample condition encoder / label projections / time MLP (6,002,304 FLOP per sample forward)
 TRAIN_FLOP_PER_SAMPLE = 3 * (FLOP_PER_SAMPLE_STEP + 6_002_304)
@@ -81,7 +123,7 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-kernel-timing', action='store_true')
     ap.add_argument('--no-extras', action='store_true',
-                    help='skip the exact-f32 rate, the MH configs[2] slice and the reference-protocol ratio')
+                    help='skip the exact-f32 and bf16x3 rates, the full MH configs[2] run and the reference-protocol ratio')
     ap.add_argument('--workload', default='iddpm', choices=['iddpm', 'mh', 'train'],
                     help='iddpm: BASELINE configs[1] (the metric); mh: configs[2] MH/SRTM2 baseline')
     ap.add_argument('--train-batch', type=int, default=256, help='training batch per GPU (main_script.py:169)')
@@ -253,11 +295,75 @@ def up0_roofline(layer_ms, bt, dtype, tflops_pipeline=None):
             'achieved': round(ach, 2), 'peak': round(peak, 2), 'unit': 'TFLOP/s', 'frac': round(ach / peak, 4),
             'traffic': pmc['traffic'], 'avg_launch_us': round(avg_s * 1e6, 2),
             'executed_tflops': round((3 if dtype == 'bf16x3' else 1) * exe * bt / avg_s / 1e12, 2)}
+    if fused_up:
+        ab = step_kernel_bytes('up0.block', dtype) * bt + weight_bytes('up0.block', dtype)
+        roof['alg_bytes'] = int(ab)
+        roof['traffic_ratio'] = round(pmc['traffic'] / ab, 2) if pmc['traffic'] else None
     if tflops_pipeline is not None:
         roof['pipeline_tflops'] = round(tflops_pipeline, 2)
-        roof['pipeline_frac'] = round(tflops_pipeline / peak, 4)
+        roof['pipeline_alg_over_peak'] = round(tflops_pipeline / peak, 4)
     roof.update(pmc_fields(pmc, avg_s))
+    kt = kernel_table(layer_ms, bt, dtype)
+    if kt is not None:
+        roof['step_kernels'] = kt
     return roof
+
+
+def load_pmc_kernels(dtype):
+    """Per-kernel PMC counters of the step kernels (profiles/pmc_traffic.json 'kernels<suffix>', written by
+    scripts/pmc_summary.py --traffic) when they were counted on this build's kernels, else None."""
+    from pet_posterior_distribution_amd import _lib
+    suf = {'bfloat16': '', 'bf16x3': '_bf16x3', 'float16': '_f16'}.get(dtype)
+    try:
+        with open(os.path.join(ROOT, 'profiles', 'pmc_traffic.json')) as f:
+            d = json.load(f).get('kernels' + suf) if suf is not None else None
+    except Exception:
+        d = None
+    now = _lib.kernel_code_hash()
+    if not d or now is None or d.get('code_hash') != now:
+        return None
+    return d
+
+
+def kernel_table(layer_ms, bt, dtype):
+    """Every step kernel of the 16-bit path against the dtype's dense MFMA peak (bf16x3: bf16 / 3):
+    mean launch time (HIP events, one eager generate at bt samples per launch), algorithmic GFLOP per
+    launch and alg_over_peak (algorithmic FLOP/s / peak: the kernels execute fewer FLOPs
+    than the reference's count -- hoisted label / time channels, folded residuals, skipped padding
+    products -- so this ratio may exceed 1), exec_frac (the MFMA FLOPs the kernel executes / peak; <= 1),
+    algorithmic bytes per launch (activations once + packed weights once) and, when the committed PMC
+    passes were taken on this build, HBM-side traffic, its ratio to the algorithmic bytes, mfma_util
+    (SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x 2.4 GHz x launch time)) and LDS bank-conflict cycles."""
+    if dtype == 'float32' or layer_ms['up0.conv2'][1] != 0:
+        return None                                   # the unfused path: the up levels run as two launches
+    peak = PEAK_BF16_TFLOPS / 3 if dtype == 'bf16x3' else PEAK_BF16_TFLOPS
+    xm = 3 if dtype == 'bf16x3' else 1
+    pk = load_pmc_kernels(dtype) if bt == 1024 else None
+    rows = []
+    for key, name, alg_mac, exe_mac in STEP_KERNELS:
+        ms, cnt = layer_ms[key]
+        if cnt == 0:
+            continue
+        avg = ms / cnt / 1e3
+        alg = 2 * alg_mac * bt
+        ab = (step_kernel_bytes(key, dtype)) * bt + weight_bytes(key, dtype)
+        r = {'kernel': name, 'timing_key': key, 'launches_per_generate': cnt, 'us': round(avg * 1e6, 2),
+             'alg_gflop': round(alg / 1e9, 3), 'alg_over_peak': round(alg / avg / 1e12 / peak, 4),
+             'exec_frac': round(xm * 2 * exe_mac * bt / avg / 1e12 / PEAK_BF16_TFLOPS, 4), 'alg_bytes': int(ab)}
+        if pk is not None:
+            c = pk['per_launch'].get(key.replace('.block', '.fused'), {})
+            if c.get('bytes'):
+                r['traffic'] = int(c['bytes'])
+                r['traffic_ratio'] = round(c['bytes'] / ab, 2)
+                r['hbm_frac'] = round(c['bytes'] / avg / 1e9 / PEAK_HBM_GBS, 4)
+            if c.get('mfma_busy_cycles'):
+                r['mfma_util'] = round(c['mfma_busy_cycles'] / (N_SIMD * PEAK_CLOCK_HZ * avg), 4)
+            if 'lds_bank_conflict_cycles' in c:
+                r['lds_bank_conflict_cycles'] = int(c['lds_bank_conflict_cycles'])
+        rows.append(r)
+    return {'peak_tflops': round(peak, 2), 'samples_per_launch': bt,
+            'pmc': None if pk is None else {'code_hash': pk['code_hash'], 'source': pk['source']},
+            'kernels': rows}
 
 
 def layer_us(layer_ms):
@@ -469,12 +575,13 @@ def f32_exact_rate(cond, B, n_rev, dev):
     m.close()
     return {'value': round(B / el, 2), 'unit': 'samples/s', 'dtype': 'f32', 'n_posterior': B,
             'reverse_steps': n_rev, 'ms_per_generate': round(el * 1e3, 2),
-            'pipeline_tflops': round(tf, 2), 'peak': PEAK_F32_TFLOPS, 'frac': round(tf / PEAK_F32_TFLOPS, 4),
+            'pipeline_tflops': round(tf, 2), 'peak': PEAK_F32_TFLOPS, 'alg_over_peak': round(tf / PEAK_F32_TFLOPS, 4),
             'executed_tflops': round(te, 2), 'executed_frac': round(te / PEAK_F32_TFLOPS, 4),
             'finite': bool(torch.isfinite(out).all()),
-            'note': 'frac: algorithmic FLOP (SURVEY 8(d): every Conv1D incl. its label/time channels and 1x1 '
-                    'residual); the kernels hoist the label/time channels into maps and fold the residual into '
-                    'the centre tap, so they execute 0.82 of that (executed_frac) and frac can exceed 1'}
+            'note': 'alg_over_peak: algorithmic FLOP (SURVEY 8(d): every Conv1D incl. its label/time channels and 1x1 '
+                    'residual) / peak; the kernels hoist the label/time channels into maps and fold the residual into '
+                    'the centre tap, so they execute 0.82 of that (executed_frac, the roofline fraction) and '
+                    'alg_over_peak can exceed 1'}
 
 
 def bf16x3_rate(cond, B, n_rev, dev):
@@ -505,25 +612,27 @@ def bf16x3_rate(cond, B, n_rev, dev):
     m.close()
     return {'value': round(B / el, 2), 'unit': 'samples/s', 'dtype': 'bf16x3 (fp32-class)', 'n_posterior': B,
             'reverse_steps': n_rev, 'ms_per_generate': round(el * 1e3, 2),
-            'pipeline_tflops': round(tf, 2), 'frac_vs_f32_peak': round(tf / PEAK_F32_TFLOPS, 4),
-            'pipeline_frac_vs_bf16x3_peak': round(tf / (PEAK_BF16_TFLOPS / 3), 4),
+            'pipeline_tflops': round(tf, 2), 'alg_over_f32_peak': round(tf / PEAK_F32_TFLOPS, 4),
+            'pipeline_alg_over_bf16x3_peak': round(tf / (PEAK_BF16_TFLOPS / 3), 4),
             'executed_bf16_tflops': round(te, 2), 'executed_frac': round(te / PEAK_BF16_TFLOPS, 4),
             'roofline': up0_roofline(lm, B, 'bf16x3'), 'layer_us': layer_us(lm),
             'finite': bool(torch.isfinite(out).all())}
 
 
-def mh_slice_and_protocol(iddpm_10k_s, dev):
-    """BASELINE configs[2] slice (10k chains x 2000 steps of the 20k) and the reference's per-TAC
-    MCMC protocol (main_script.py:363-364, pymc's default 4 chains: 4 x (20k draws + 40k tune)),
-    timed as a 1/10 slice x 10; ratio against iDDPM's 10,000 posterior samples of one TAC
+def mh_config2_and_protocol(iddpm_10k_s, dev, cpu=True):
+    """BASELINE configs[2] at full size -- 48 ROI x 10k chains x 20k steps (10k tune + 10k draws), fp64,
+    about 16 s -- with its fp64 roofline and the oracle/mh_ref.c CPU baseline (rank 0, bounded sample); and
+    the reference's per-TAC MCMC protocol (main_script.py:363-364, pymc's default 4 chains: 4 x (20k draws
+    + 40k tune)), timed as a 1/10 slice x 10, against iDDPM's 10,000 posterior samples of one TAC
     (main_script.py:315-319) on the same GPU -- the README.md:12 '> 230x' claim, same silicon."""
     import torch
     from pet_posterior_distribution_amd.mcmc import MetropolisSRTM2
     from pet_posterior_distribution_amd.sim_data import mh_problem
-    mh = MetropolisSRTM2(**mh_problem(seed=0))
+    P = mh_problem(seed=0)
+    mh = MetropolisSRTM2(**P)
     mh.run(512, 2, 0, seed=1)
     torch.cuda.synchronize()
-    n, tune, draws = 10000, 1000, 1000      # about 1.6 s: long enough that run set-up is < 2 %
+    n, tune, draws = 10000, 10000, 10000
     t0 = time.perf_counter()
     res = mh.run(n, draws, tune, seed=7)
     torch.cuda.synchronize()
@@ -535,9 +644,13 @@ def mh_slice_and_protocol(iddpm_10k_s, dev):
     torch.cuda.synchronize()
     proto = (time.perf_counter() - t1) * 10
     mh.close()
-    return ({'value': round(steps / el, 1), 'unit': 'chain-steps/s', 'chains': n, 'steps_per_chain': tune + draws,
-             'seconds': round(el, 3), 'fp64_tflops': round(fl, 2), 'frac': round(fl / 78.6, 4),
-             'mean_accept_rate': round(float(res['accept_rate'].mean()), 4)},
+    cfg2 = {'value': round(steps / el, 1), 'unit': 'chain-steps/s', 'chains': n, 'steps_per_chain': tune + draws,
+            'tune': tune, 'draws': draws, 'seconds': round(el, 3), 'dtype': 'f64',
+            'roofline': {'bound': 'valu-fp64', 'achieved': round(fl, 2), 'peak': 78.6, 'unit': 'TFLOP/s',
+                         'frac': round(fl / 78.6, 4), 'traffic': None, 'flop_per_update': MH_FP64_FLOP_PER_UPDATE},
+            'mean_accept_rate': round(float(res['accept_rate'].mean()), 4),
+            'cpu_baseline': mh_cpu_baseline(P) if cpu else None}
+    return (cfg2,
             {'mh_protocol_s_per_tac': round(proto, 3), 'mh_protocol': '4 chains x (20000 draws + 40000 tune), '
              'timed as 4 x (2000 + 4000) x 10', 'iddpm_s_per_tac': round(iddpm_10k_s, 3),
              'iddpm_protocol': '10,000 posterior samples x 1000 reverse steps, bf16, one launch',
@@ -717,7 +830,8 @@ def main():
             line['f32_exact'] = f32_exact_rate(cond[0], B, n_rev, dev)
             line['bf16x3'] = bf16x3_rate(cond[0], B, n_rev, dev)
             t10k = iddpm_10k_seconds(model, cond[0])
-            line['mh_config3_slice'], line['reference_protocol'] = mh_slice_and_protocol(t10k, dev)
+            line['mh_config2'], line['reference_protocol'] = mh_config2_and_protocol(t10k, dev,
+                                                                                     not args.no_cpu_baseline)
             line['weights_sensitivity'] = weights_sensitivity(net, cond[0], B, dev)
         sm = allst[..., 1]
         line['posterior_mean_DVR_roi0'] = [round(float(v), 5) for v in sm[:, 0, 0]]

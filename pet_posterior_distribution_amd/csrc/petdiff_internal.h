@@ -139,23 +139,12 @@ constexpr TileCfg layer_tile(int kind) {
                                                                                   : TileCfg{4, 1, 3, 64};
 }
 constexpr int layer_ntile(int kind) { return 64 * layer_tile(kind).wn; }
-// bf16x3 K chunks on the 64-B-row layers (down2, down3, up0 / up1 fused, the unfused up blocks):
-// 1 = paired, a chunk holds 16 channels as [hi(16) | lo(16)] of both operands and runs the three
-// products (a_hi, w_hi), (a_hi, w_lo), (a_lo, w_hi) on it, so each byte is staged once (2 x the bf16
-// chunks); 0 = three passes over the channels, (a_hi, w_hi) then (a_hi, w_lo) then (a_lo, w_hi), with
-// a_hi and w_hi staged twice (3 x the bf16 chunks).  down1 keeps the three passes: the final level's
-// fused next-step down1 walks its packed weights in that order.
-#ifndef CONV_X3_PAIRED
-#define CONV_X3_PAIRED 1
-#endif
-// down2 / down3 separately (their loader waves hide most of the stream; A/B switch)
-#ifndef CONV_X3_PAIRED_PM
-#define CONV_X3_PAIRED_PM 1
-#endif
-constexpr bool x3_paired(int kind) {
-  return CONV_X3_PAIRED && layer_tile(kind).rowb == 64 && kind != LK_DOWN1 &&
-         (CONV_X3_PAIRED_PM || (kind != LK_DOWN2 && kind != LK_DOWN3));
-}
+// bf16x3 K chunks on the 64-B-row layers (down1, down2, down3, up0 / up1 fused, the unfused up blocks) are
+// paired: a chunk holds 16 channels as [hi(16) | lo(16)] of both operands and runs the three products
+// (a_hi, w_hi), (a_hi, w_lo), (a_lo, w_hi) on it, so each byte is staged once (2 x the bf16 chunks).  The
+// 32-B-row final level walks three passes over the channels, (a_hi, w_hi) then (a_hi, w_lo) then
+// (a_lo, w_hi), staging a_hi and w_hi twice (3 x the bf16 chunks).
+constexpr bool x3_paired(int kind) { return layer_tile(kind).rowb == 64; }
 template <typename T>
 constexpr int layer_kc(int kind) { return layer_tile(kind).rowb / (int)sizeof(T); }
 

@@ -11,11 +11,16 @@ LAYERS = ['down1', 'down2', 'down3', 'up0.conv2', 'up0.block', 'up1.conv2', 'up1
 def label(name):
     if 'down0_kernel' in name:
         return 'down0'
+    # rocprofv3's demangler garbles the bf16 instances of kinds 1 and 2 (down2, down3):
+    # conv_kernel<bf16, 1, XS> -> 'conv_kernel<bool _Accum, int, E, XS>',
+    # conv_kernel<bf16, 2, 1> -> 'conv_kernel<bool _Accum, int, EL, int, E>'
+    if re.search(r'conv_kernel<bool _Accum, int, EL, int, E>', name):
+        return 'down3'
+    if re.search(r'conv_kernel<bool _Accum, int, E(, \d+)?>', name):
+        return 'down2'
     m = re.search(r'conv_kernel.*?Li(\d+)E', name) or re.search(r'conv_kernel<[^,]*, (\d+)>', name)
-    if 'conv_kernel' in name:
-        if m:
-            return LAYERS[int(m.group(1))]
-        return 'down2'          # the demangler garbles the <bf16, 1> instance
+    if 'conv_kernel' in name and m:
+        return LAYERS[int(m.group(1))]
     return None
 
 

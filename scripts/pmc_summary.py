@@ -27,6 +27,8 @@ def short(name):
     # launches (0, 1, 2, 9, 10, 11) only kind 1 (down2) comes out that way
     if re.search(r'conv_kernel<bool _Accum, int, E(, \d+)?>', name):
         return 'down2'
+    if re.search(r'conv_kernel<bool _Accum, int, EL, int, E>', name):   # conv_kernel<bf16, 2, 1> (bf16x3 down3)
+        return 'down3'
     return None
 
 
@@ -73,6 +75,19 @@ def main(d, out=None, update_traffic=False, dtype='bfloat16'):
             for c, name in (('SQ_VALU_MFMA_BUSY_CYCLES', '_mfma_busy_cycles'), ('GRBM_GUI_ACTIVE', '_grbm_gui_active')):
                 if c in ub:
                     tr[pre + name] = ub[c]
+        # every step kernel's counters (bench.py's per-kernel roofline table), stamped with the build
+        ks = {}
+        for key, ub in res.items():
+            row = {}
+            if 'hbm_read_bytes_corrected' in ub and 'hbm_write_bytes' in ub:
+                row['bytes'] = ub['hbm_read_bytes_corrected'] + ub['hbm_write_bytes']
+            for c, name in (('SQ_VALU_MFMA_BUSY_CYCLES', 'mfma_busy_cycles'), ('GRBM_GUI_ACTIVE', 'grbm_gui_active'),
+                            ('SQ_LDS_BANK_CONFLICT', 'lds_bank_conflict_cycles'), ('SQ_WAIT_ANY', 'sq_wait_any'),
+                            ('SQ_BUSY_CYCLES', 'sq_busy_cycles')):
+                if c in ub:
+                    row[name] = ub[c]
+            ks[key] = row
+        tr['kernels' + suf] = {'code_hash': code_hash, 'source': os.path.relpath(out, root), 'per_launch': ks}
         tr['method'] = 'rocprofv3 --pmc FETCH_SIZE (x2, gfx950 64-B tally) + WRITE_SIZE, KB->B, mean per dispatch'
         json.dump(tr, open(tp, 'w'), indent=1)
     return res

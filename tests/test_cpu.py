@@ -448,6 +448,38 @@ def test_bench_pmc_fields_per_dtype_and_build(monkeypatch):
         assert pmc['stale'] and pmc['traffic'] is None
 
 
+def test_bench_step_kernel_table(monkeypatch):
+    """bench.py's roofline lists all 6 step kernels of the 16-bit path: launch time,
+    algorithmic GFLOP, alg_over_peak, exec_frac (executed MFMA FLOPs / peak) and algorithmic
+    bytes; PMC-derived traffic / mfma_util / LDS conflicts only when the committed passes match the build.
+    No field named frac exceeds 1 at the kernels' measured speeds, and the App. A MACs add up to the
+    SURVEY total."""
+    import bench
+    from pet_posterior_distribution_amd import _lib
+    tot = sum(k[2] for k in bench.STEP_KERNELS) + 48 * 7 * 52 * 128 * 0
+    # App. A total (148.18 M MAC) = down0 + the 6 kernels' counts (up2's includes the next step's down0)
+    assert tot == bench.FLOP_PER_SAMPLE_STEP // 2
+    us = {'down0': 0, 'down1': 13.4, 'down2': 18.3, 'down3': 25.6, 'up0.block': 59.7, 'up1.block': 37.6,
+          'up2.block': 40.1}
+    lm = {k: (0.0, 0) for k in ('down0', 'down1', 'down2', 'down3', 'up0.conv2', 'up0.block', 'up1.conv2',
+                                 'up1.block', 'up2.conv2', 'up2.block')}
+    for k, u in us.items():
+        lm[k] = (u * 1e-3 * 1000, 1000 if u else 0)
+    monkeypatch.setattr(_lib, 'kernel_code_hash', lambda *a, **k: 'no such build')
+    lm3 = {k: (v[0] * 2.6, v[1]) for k, v in lm.items()}     # bf16x3 runs about 2.6 x the bf16 times
+    for dt, lmd in (('bfloat16', lm), ('bf16x3', lm3)):
+        kt = bench.kernel_table(lmd, 1024, dt)
+        assert [r['timing_key'] for r in kt['kernels']] == ['down1', 'down2', 'down3', 'up0.block', 'up1.block',
+                                                              'up2.block']
+        assert kt['pmc'] is None and all('mfma_util' not in r for r in kt['kernels'])
+        for r in kt['kernels']:
+            assert 0 < r['exec_frac'] < 1 and r['alg_bytes'] > 0
+    r = {x['timing_key']: x for x in bench.kernel_table(lm, 1024, 'bfloat16')['kernels']}
+    assert abs(r['up0.block']['alg_gflop'] - 117.23) < 0.01 and abs(r['up0.block']['alg_over_peak'] - 0.786) < 0.001
+    assert abs(r['down3']['alg_gflop'] - 49.50) < 0.01
+    assert bench.kernel_table({**lm, 'up0.conv2': (1.0, 1000)}, 1024, 'bfloat16') is None   # unfused path
+
+
 def test_reference_prior_fixture():
     """G0: the arrays of the reference's prior_stats_nROI48.pik (sample_sim_data.py:106-126), read by
     tests/golden/make_golden.py without unpickling; the package ships an identical copy
