@@ -131,6 +131,7 @@ struct petdiff_ctx {
   DevBuf w32;                        // fp32 Keras blob on device
   DevBuf wpack[kNumConvLayers];      // packed conv weights (bf16 or f32)
   DevBuf w0;                         // down0 x weights [6][2][128] fp32 (res folded)
+  DevBuf wf4;                        // final Conv1D kernel as [128][4] fp32, zero-padded (FinalArgs::wf4)
   DevBuf bias_only[kNumConvLayers];  // conv bias + res bias for up blocks
   DevBuf tmap[7], cmap[7];           // per cond level
   // fused up levels (16-bit path; PETDIFF_FUSE_UP=0 keeps the separate k2-conv launches)
@@ -151,6 +152,7 @@ struct petdiff_ctx {
   // run the next step's down0 inside the previous step's up2.block epilogue (generate);
   // PETDIFF_FUSE_DOWN0=0 restores the standalone down0 launch per step (A/B switch)
   bool fuse_down0 = true;
+  bool up2_x3_paired = true;         // bf16x3: the final level on paired 64-B chunks (LK_UP2_FX3)
   DevBuf xa, xb, tacbuf, tbuf, rng;
   hipStream_t cap_stream = nullptr;
   int seg_steps = 0;                   // reverse steps per captured graph segment (0: the whole loop)
@@ -270,13 +272,18 @@ const FusedLevel kFused[3] = {
     {LK_UP2_F, LK_UP2_CONV2, LK_UP2_BLOCK, 6, 48, 128, 256, 128},
 };
 
+// kernel kind of fused level u (the bf16x3 network's final level runs its paired-chunk instance)
+// (PETDIFF_UP2_X3_PAIRED=0: the three-pass 32-B-row instance, an A/B switch read at create)
+int fused_kind(const petdiff_ctx* h, int u) { return (u == 2 && h->x3 && h->up2_x3_paired) ? LK_UP2_FX3 : kFused[u].kind; }
+
 // Weights of a fused up level: per N tile, the block's skip-half chunks [6 taps][NT][ROWB]
 // (residual folded into tap 2) then the coarse-input chunks [phase][4 taps][NT][ROWB] of the
 // composite taps (compose_kernel), both with the 16-B pieces XOR-swizzled by n; plus the
 // left-edge correction weights [n_tile][chunk][phase][NT][KC] (plain).
 template <typename T, typename H>
 int pack_fused(petdiff_ctx* h, const std::vector<float>& host, int u) {
-  const FusedLevel& fl = kFused[u];
+  FusedLevel fl = kFused[u];
+  fl.kind = fused_kind(h, u);
   const ConvLayer& blk = kConv[fl.block_li];
   const ConvLayer& c2 = kConv[fl.conv2_li];
   const int ROWB = layer_tile(fl.kind).rowb, KC = layer_kc<T>(fl.kind), NT = layer_ntile(fl.kind);
@@ -509,7 +516,7 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
           a.fin.next.s0 = s0_other;
         }
       }
-      CHK(timed(1 + li, [&] { return launch_conv<T>(fl.kind, a, s, h->x3); }));
+      CHK(timed(1 + li, [&] { return launch_conv<T>(fused_kind(h, u), a, s, h->x3); }));
       continue;
     }
     ConvArgs<T> a{};
@@ -563,6 +570,7 @@ int network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
 FinalArgs base_final(petdiff_ctx* h) {
   FinalArgs f{};
   f.wf = h->W("final.kernel");
+  f.wf4 = h->wf4.as<float>();
   f.bf = h->W("final.bias");
   f.n_out = h->n_out;
   f.tab = h->tab.as<float>();
@@ -648,6 +656,7 @@ int petdiff_create(const petdiff_config* cfg, const float* weights, size_t n_wei
   h->x3 = cfg->dtype == PETDIFF_DTYPE_BF16X3;
   h->spec = make_spec(*cfg, h->n_out);
   if (const char* e = std::getenv("PETDIFF_FUSE_DOWN0")) h->fuse_down0 = std::atoi(e) != 0;
+  if (const char* e = std::getenv("PETDIFF_UP2_X3_PAIRED")) h->up2_x3_paired = std::atoi(e) != 0;
   h->fuse_up = cfg->dtype != PETDIFF_DTYPE_F32;
   if (const char* e = std::getenv("PETDIFF_FUSE_UP")) h->fuse_up = h->fuse_up && std::atoi(e) != 0;
   const size_t need = h->spec.back().off + h->spec.back().size;
@@ -694,6 +703,14 @@ int petdiff_create(const petdiff_config* cfg, const float* weights, size_t n_wei
         }
     HIPC(h->w0.alloc(w0.size() * 4));
     HIPC(hipMemcpy(h->w0.p, w0.data(), w0.size() * 4, hipMemcpyHostToDevice));
+  }
+  {
+    std::vector<float> wf4(128 * 4, 0.f);
+    const float* wf = host.data() + h->off.at("final.kernel");
+    for (int n = 0; n < 128; ++n)
+      for (int o = 0; o < h->n_out; ++o) wf4[n * 4 + o] = wf[n * h->n_out + o];
+    HIPC(h->wf4.alloc(wf4.size() * 4));
+    HIPC(hipMemcpy(h->wf4.p, wf4.data(), wf4.size() * 4, hipMemcpyHostToDevice));
   }
   *out = h.release();
   return PETDIFF_OK;

@@ -41,6 +41,7 @@ struct Down0Args {
 
 struct FinalArgs {
   const float* wf;     // [128][n_out] final Conv1D 1x1 kernel
+  const float* wf4;    // the same as [128][4], zero-padded when n_out == 2 (16-B rows for the fused final level)
   const float* bf;     // [n_out]
   int n_out;           // 4 (learned variance) or 2
   const float* x_t;    // [B][n_roi][2] current sample
@@ -122,7 +123,10 @@ enum LayerKind : int {
   // Fused up levels (16-bit path): UpSampling1D -> Conv1D(k2) -> concat -> ConvBlock as ONE
   // implicit GEMM.  The k2 conv is linear, so it composes with the block's k6 conv into a
   // 2-phase (even / odd output position) 4-tap conv on the coarse input; see DESIGN.md.
-  LK_UP0_F = kNumConvLayers, LK_UP1_F, LK_UP2_F, kNumKinds
+  LK_UP0_F = kNumConvLayers, LK_UP1_F, LK_UP2_F,
+  // the final fused level of the bf16x3 network: paired [hi | lo] 64-B chunks on a 2-stage ring (the
+  // 32-B rows of LK_UP2_F cannot hold a 16-channel pair; 3 stages of 64-B rows exceed the LDS)
+  LK_UP2_FX3, kNumKinds
 };
 constexpr bool is_fused_kind(int kind) { return kind >= LK_UP0_F && kind < kNumKinds; }
 
@@ -132,9 +136,16 @@ constexpr bool is_fused_kind(int kind) { return kind >= LK_UP0_F && kind < kNumK
 struct TileCfg {
   int wm, wn, stages, rowb;
 };
+// Co-residency experiment (scripts/micro/coresident.sh): down1 on a 2-stage ring of
+// 32-B chunks, about 61 KB of LDS and 186 VGPRs, so two workgroups share a CU.  Product builds use 0.
+#ifndef CONV_DOWN1_CORES
+#define CONV_DOWN1_CORES 0
+#endif
 constexpr TileCfg layer_tile(int kind) {
-  return kind == LK_UP2_BLOCK ? TileCfg{2, 2, 2, 64}                // final conv needs all 128 channels
+  return CONV_DOWN1_CORES && kind == LK_DOWN1 ? TileCfg{4, 1, 2, 32}
+         : kind == LK_UP2_BLOCK ? TileCfg{2, 2, 2, 64}                // final conv needs all 128 channels
          : kind == LK_UP2_F ? TileCfg{2, 2, 3, 32}                 // + 2-phase B tiles: 3 x 32-B chunks
+         : kind == LK_UP2_FX3 ? TileCfg{2, 2, 2, 64}               // bf16x3: 2 x 64-B paired chunks
          : (kind == LK_UP0_CONV2 || kind == LK_UP1_CONV2 || kind == LK_UP2_CONV2) ? TileCfg{4, 1, 3, 128}
                                                                                   : TileCfg{4, 1, 3, 64};
 }

@@ -26,6 +26,11 @@
 #ifndef CONV_LOADERS
 #define CONV_LOADERS 1
 #endif
+// The fused final level's time / label map rows: 1 = staged in LDS by LDS-DMA at kernel start, 0 = read
+// from L2 in the epilogue (A/B switch)
+#ifndef CONV_FIN_LDS_MAPS
+#define CONV_FIN_LDS_MAPS 1
+#endif
 
 // Diagnostic builds only (scripts/micro/conv_micro.hip): bit 1 drops the K-loop DMA,
 // bit 2 the MFMAs, bit 4 the epilogue, bit 8 returns at entry, bit 16 returns after
@@ -79,6 +84,14 @@ __device__ __forceinline__ f32x16 mfma32(f16x8 a, f16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+// TR: the transposed product C^T += B^T A^T (the operands' roles swapped), so the accumulator of a 32 x 32
+// tile holds one tile ROW per lane and 16 output channels in its registers (the final level's
+// register-direct final conv).  Each output element takes the same products in the same k order.
+template <bool TR, typename F>
+__device__ __forceinline__ f32x16 mfma_ab(F a, F b, f32x16 c) {
+  if constexpr (TR) return mfma32(b, a, c);
+  else return mfma32(a, b, c);
+}
 
 
 __device__ __forceinline__ float to_f(float v) { return v; }
@@ -231,6 +244,7 @@ template <> struct LayerShape<LK_UP2_BLOCK> { static constexpr int L = 48, TAPS 
 template <> struct LayerShape<LK_UP0_F> { static constexpr int L = 12, TAPS = 6, PADL = 2, EPI = EPI_RELU; static constexpr bool UPS = false, FUSED = true; };
 template <> struct LayerShape<LK_UP1_F> { static constexpr int L = 24, TAPS = 6, PADL = 2, EPI = EPI_RELU; static constexpr bool UPS = false, FUSED = true; };
 template <> struct LayerShape<LK_UP2_F> { static constexpr int L = 48, TAPS = 6, PADL = 2, EPI = EPI_FINAL; static constexpr bool UPS = false, FUSED = true; };
+template <> struct LayerShape<LK_UP2_FX3> : LayerShape<LK_UP2_F> {};
 
 // launch-bound threads: 8 waves (4 MFMA + 4 loader) or 4 (fused layers)
 template <int KIND> constexpr int conv_max_threads() { return is_fused_kind(KIND) ? kThreads : 2 * kThreads; }
@@ -340,8 +354,10 @@ struct ConvGeom {
   static constexpr int CT_LD = 2 * NT + 8;          // fp32 C tile, one ROW PAIR [c][2] per line (non-final)
   static constexpr int FIN_LD = 132;                // fp32 C tile row (final epilogue, 16-B aligned)
   // FINAL: C tile | final kernel [128][4] | x_next rows [MT][2] (fused next-step down0)
+  // the non-final C tile is staged in EPI_PARTS row blocks (co-residency experiment: 2, half the LDS)
+  static constexpr int EPI_PARTS = (CONV_DOWN1_CORES && KIND == LK_DOWN1) ? 2 : 1;
   static constexpr int EPI_BYTES =
-      (EPI == EPI_FINAL) ? MT * FIN_LD * 4 + 128 * 4 * 4 + MT * 2 * 4 + 64 : (MT / 2) * CT_LD * 4;
+      (EPI == EPI_FINAL) ? MT * FIN_LD * 4 + 128 * 4 * 4 + MT * 2 * 4 + 64 : (MT / 2 / EPI_PARTS) * CT_LD * 4;
   static constexpr int RING = STAGES * STAGE;
   // Non-final epilogues: the block's time map [L][NT] and label map [L][NT] (fp32) and
   // the condition index of its samples are prefetched into LDS behind the ring at
@@ -349,7 +365,7 @@ struct ConvGeom {
   static constexpr bool PREMAP = EPI != EPI_FINAL;
   static constexpr int MAP_PIECES = L * NT / 4;                       // 16-B pieces of one map
   static constexpr int C_PIECE0 = (MAP_PIECES + 63) / 64 * 64;        // label map starts wave-instr aligned
-  static constexpr int MAP_OFF = RING;
+  static constexpr int MAP_OFF = (EPI_PARTS > 1 && EPI_BYTES > RING) ? (EPI_BYTES + 255) / 256 * 256 : RING;
   // map pieces per wave when every wave issues the same count (fused levels: the first ring barrier
   // then waits for chunk 0 only, vmcnt(NPI_MAP)); the region is padded to whole block instructions
   static constexpr int NPI_MAP = (C_PIECE0 + MAP_PIECES + kThreads - 1) / kThreads;
@@ -361,17 +377,19 @@ struct ConvGeom {
   // fused final level: its time and label map rows [L][FIN_LD] fp32 (padded rows: the row loop's
   // lanes read consecutive rows conflict-free) prefetched behind the ring at kernel start
   static constexpr bool FIN_MAPS = FUSED && EPI == EPI_FINAL;
+  // ... their map rows staged in LDS at kernel start (CONV_FIN_LDS_MAPS=0: the epilogue reads them from L2)
+  static constexpr bool FIN_LDS = FIN_MAPS && CONV_FIN_LDS_MAPS && ROWB == 32;
   static constexpr int FMAP_PIECES = L * (FIN_LD / 4);                 // per map, incl. one pad piece per row
   // both maps as one array of 2 FMAP_PIECES pieces: every wave issues FMAP_FULL block instructions,
   // waves with wv * 64 < FMAP_REM one more (its lanes past the end land in the padding)
   static constexpr int FMAP_STRIDE = FMAP_PIECES;                      // pieces between the two maps
   static constexpr int FMAP_FULL = 2 * FMAP_PIECES / kThreads, FMAP_REM = 2 * FMAP_PIECES - FMAP_FULL * kThreads;
   static constexpr int FMAP_OFF = (SMEM0 + 15) / 16 * 16;
-  static constexpr int FMAP_BYTES = FIN_MAPS ? (FMAP_FULL * kThreads + (FMAP_REM + 63) / 64 * 64) * 16 : 0;
+  static constexpr int FMAP_BYTES = FIN_LDS ? (FMAP_FULL * kThreads + (FMAP_REM + 63) / 64 * 64) * 16 : 0;
   static constexpr int SMEM1 = SMEM0 > TAIL ? SMEM0 : TAIL;
   static constexpr int SMEM = FIN_MAPS ? FMAP_OFF + FMAP_BYTES : SMEM1;
   static_assert(!FIN_MAPS || (TAIL == 0 && FIN_LD == 132 && NT == 128), "final map layout");
-  static_assert(!PREMAP || EPI_BYTES <= RING, "C tile must not overlap the prefetched maps");
+  static_assert(!PREMAP || EPI_BYTES <= MAP_OFF, "C tile must not overlap the prefetched maps");
   // Dedicated loader waves (16-bit 3-stage layers): 4 extra waves issue every LDS-DMA
   // piece, so the 4 MFMA waves never stall on DMA issue.
   // (not the fused layers: 4 waves per workgroup leave them the whole 512-entry register file
@@ -384,7 +402,7 @@ struct ConvGeom {
   static_assert(!PM || (CONV_LOADERS && STAGES == 3), "position-major layers run on the loader-wave ring");
   static_assert(MT % L == 0, "tile must hold whole samples");
   static_assert(B_BYTES % (16 * kThreads) == 0, "B tile split");
-  static_assert(ROWB == 64 || ROWB == 128 || (ROWB == 32 && FUSED), "row width");
+  static_assert(ROWB == 64 || ROWB == 128 || (ROWB == 32 && (FUSED || STAGES == 2)), "row width");
   static_assert(STAGES == 2 || (STAGES == 3 && AFULL && AFULL2), "3-stage ring needs uniform per-wave DMA counts");
   static_assert(PER < 64 && PER2 < 64, "vmcnt range");
   static_assert(!FUSED || (PHROWS % 96 == 0 && S % 2 == 0 && S <= 32 && B2_BYTES % (16 * kThreads) == 0),
@@ -797,6 +815,9 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   const int m0 = m_tile * G::S;
 
   constexpr bool P3 = DmaPlan<T, KIND, XS>::P3;     // paired bf16x3 chunks (x3_paired)
+  // fused final level: transposed accumulators (mfma_ab), one tile row per lane, so the final 1x1 conv
+  // runs from the registers without staging the C tile (the unfused final level keeps the staged rows)
+  constexpr bool TF = G::FIN_MAPS;
   const int NC = P3 ? (a.c1 + a.c2) / (G::KC / 2) : (XS ? 3 : 1) * (a.c1 / G::KC + a.c2 / G::KC);
 
   // Final level: this thread's output row (one per thread) and every global operand of its
@@ -983,7 +1004,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
 #pragma unroll
       for (int jn = 0; jn < 2; ++jn)
         if constexpr (sizeof(T) == 2 && !(CONV_EXP_MODE & 2))
-          acc[i][jn] = mfma32(av[pb][i], bv[pb][jn], acc[i][jn]);
+          acc[i][jn] = mfma_ab<TF>(av[pb][i], bv[pb][jn], acc[i][jn]);
   };
   // Fused: left-edge correction weights of this lane (registers, one chunk ahead), see has_m0
   constexpr int NGE = G::FUSED ? ROWB / 32 : 1;
@@ -1279,7 +1300,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         const int pb = sb ^ 1;
 #define PETDIFF_MF(i, jn)                                                                                  \
   if constexpr (!(CONV_EXP_MODE & 2))                                                                      \
-    acc[i][jn] = mfma32(av[pb][i], bv[pb][jn], acc[i][jn]);
+    acc[i][jn] = mfma_ab<TF>(av[pb][i], bv[pb][jn], acc[i][jn]);
 #define PETDIFF_RD(dst, ptr) \
   if constexpr (!(CONV_EXP_MODE & 64)) dst = *reinterpret_cast<const fragT*>(ptr);
         PETDIFF_MF(0, 0)
@@ -1312,7 +1333,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
             for (int gg = 0; gg < NG; ++gg)
 #pragma unroll
               for (int jn = 0; jn < 2; ++jn)
-                if constexpr (!(CONV_EXP_MODE & 2)) acc[0][jn] = mfma32(am[kg_a<P3>(gg) >> 5], epk[kg_b<P3>(gg) >> 5][jn], acc[0][jn]);
+                if constexpr (!(CONV_EXP_MODE & 2)) acc[0][jn] = mfma_ab<TF>(am[kg_a<P3>(gg) >> 5], epk[kg_b<P3>(gg) >> 5][jn], acc[0][jn]);
             const int k2 = kc - dma.n1;
             if (kc + 1 < NC) load_epk(k2 + 1);
           }
@@ -1447,14 +1468,14 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   // fused final level, t uniform and one condition in the tile: map rows into LDS (FMAP_OFF)
   bool fin_fast = false;
   int tac0f = 0;
-  if constexpr (G::FIN_MAPS) {   // read before any DMA is issued: waiting on them retires nothing else
+  if constexpr (G::FIN_LDS) {    // read before any DMA is issued: waiting on them retires nothing else
     tac0f = a.tac ? a.tac[min(m0, B - 1)] : 0;
     fin_fast = a.t_uniform >= 0 && a.tmap && a.cmap;
     if (a.tac)
       for (int k = 1; k < G::S; ++k) fin_fast = fin_fast && (m0 + k >= B || a.tac[m0 + k] == tac0f);
   }
   auto prefetch_fin_maps = [&]() {
-    if constexpr (G::FIN_MAPS) {
+    if constexpr (G::FIN_LDS) {
       const i32x4 rs_t = make_rsrc(a.tmap, (unsigned)a.n_t * L * (unsigned)a.cout * 4u);
       const i32x4 rs_c = make_rsrc(a.cmap, (unsigned)a.n_tac * L * (unsigned)a.cout * 4u);
       // a fixed number of instructions per wave (the first ring barrier counts them); pieces past
@@ -1476,8 +1497,8 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   };
   // LDS-DMA instructions per wave issued by the two prefetches (fused levels): NMAPW, or NMAPW + 1
   // for the waves that issue the final maps' partial instruction
-  constexpr int NMAPW = (G::PREMAP && G::FUSED ? G::NPI_MAP : 0) + (G::FIN_MAPS ? G::FMAP_FULL : 0);
-  const bool map_extra = G::FIN_MAPS && wv * 64 < G::FMAP_REM;
+  constexpr int NMAPW = (G::PREMAP && G::FUSED ? G::NPI_MAP : 0) + (G::FIN_LDS ? G::FMAP_FULL : 0);
+  const bool map_extra = G::FIN_LDS && wv * 64 < G::FMAP_REM;
   using Seg2Next = std::integral_constant<int, 3>;
   if constexpr (G::FUSED) {
     // Fused up level: segment-1 chunks (skip s), then segment-2 chunks (coarse b); every
@@ -1728,6 +1749,15 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     // The tile interleaves row pairs ([r/2][c][2]): an accumulator's consecutive rows
     // (rg, rg+1) go out as one ds_write_b64 and a row pair comes back as 4 ds_read_b128.
     float* ct = reinterpret_cast<float*>(smem);
+    static_assert(G::EPI_PARTS == 1 || (!G::PM && !G::W6 && !G::FUSED && G::WN == 1), "row-block staging");
+    constexpr int PROWS = G::MT / G::EPI_PARTS;        // tile rows staged per part
+#if CONV_DOWN1_CORES
+    auto stage_c = [&](auto part_tag) {
+    constexpr int part = decltype(part_tag)::value;
+    if (G::EPI_PARTS == 1 || wm / (G::WM / G::EPI_PARTS) == part)
+#else
+    constexpr int part = 0;
+#endif
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -1738,10 +1768,14 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
           // PW6: fragment f = 3 jn + i is position pw6_pos(pw6set, f) of sample half pw6_sh, at its PM tile row
           const int r = (G::W6    ? w6e * G::PHROWS + (3 * jn + i) * G::S
                          : G::PM ? G::pm_row(G::pw6_pos(pw6set, 3 * jn + i), G::pw6_sh(pw6set) * 32)
-                                  : G::frag_row(wm, i)) + (rg & 3) + 8 * (rg >> 2) + 4 * h;   // even
+                                  : G::frag_row(wm, i)) + (rg & 3) + 8 * (rg >> 2) + 4 * h - part * PROWS;
           *reinterpret_cast<float2*>(ct + (r >> 1) * G::CT_LD + (G::W6 || G::PM ? w6h * 32 + lr : wn * 64 + jn * 32 + lr) * 2) =
               make_float2(acc[i][jn][rg], acc[i][jn][rg + 1]);
         }
+#if CONV_DOWN1_CORES
+    };
+    stage_c(std::integral_constant<int, 0>{});
+#endif
     __syncthreads();
 #if CONV_EXP_MODE & 128
     if (tid == 0) reinterpret_cast<unsigned long long*>(a.fin.x_all)[4096 + 2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
@@ -1755,8 +1789,13 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     // (a load on any path would make the compiler drain the stores with vmcnt(0))
     // MODE 1: time + label maps from LDS; 2: bias only (registers); 0: general (global loads)
     const int mode = (pre_t && pre_c && stac[G::S] == 0) ? 1 : (!a.tmap && !a.cmap) ? 2 : 0;
-    static_assert((G::MT / 2) % (kThreads / TPR) == 0, "row pairs split evenly");
+    static_assert((G::MT / 2 / G::EPI_PARTS) % (kThreads / TPR) == 0, "row pairs split evenly");
+#if CONV_DOWN1_CORES
+    auto epi_rows = [&](auto mode_tag, auto part_tag) {
+      constexpr int part = decltype(part_tag)::value;
+#else
     auto epi_rows = [&](auto mode_tag) {
+#endif
       constexpr int MODE = decltype(mode_tag)::value;
       constexpr bool FAST = MODE != 0;
       constexpr bool SPAIR = G::FUSED || G::PM;   // a row pair is two samples at one position
@@ -1765,7 +1804,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       auto pair = [&](int rp, int s, int l, float (&v)[2][8]) {
         f32x4 cq[4];   // (r, r+1) x channels nloc .. nloc+7, interleaved
 #pragma unroll
-        for (int k = 0; k < 4; ++k) cq[k] = *reinterpret_cast<const f32x4*>(ct + rp * G::CT_LD + nloc * 2 + 4 * k);
+        for (int k = 0; k < 4; ++k) cq[k] = *reinterpret_cast<const f32x4*>(ct + (rp - part * PROWS / 2) * G::CT_LD + nloc * 2 + 4 * k);
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
           const int se = SPAIR ? s + e : s, le = SPAIR ? l : l + e, be = m0 + se;
@@ -1824,7 +1863,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         }
       } else {
 #pragma unroll
-        for (int rp = tid / TPR; rp < G::MT / 2; rp += kThreads / TPR) {
+        for (int rp = part * PROWS / 2 + tid / TPR; rp < (part + 1) * PROWS / 2; rp += kThreads / TPR) {
           const int r = 2 * rp;
           int s, l;
           G::row_sl(r, s, l);
@@ -1842,9 +1881,22 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         }
       }
     };
+#if CONV_DOWN1_CORES
+    static_for<0, G::EPI_PARTS>([&](auto part_tag) {
+      if constexpr (decltype(part_tag)::value > 0) {  // the next row block: every read of the last one done
+        __syncthreads();
+        stage_c(part_tag);
+        __syncthreads();
+      }
+      if (mode == 1) epi_rows(std::integral_constant<int, 1>{}, part_tag);
+      else if (mode == 2) epi_rows(std::integral_constant<int, 2>{}, part_tag);
+      else epi_rows(std::integral_constant<int, 0>{}, part_tag);
+    });
+#else
     if (mode == 1) epi_rows(std::integral_constant<int, 1>{});
     else if (mode == 2) epi_rows(std::integral_constant<int, 2>{});
     else epi_rows(std::integral_constant<int, 0>{});
+#endif
 #if CONV_EXP_MODE & 128
     if (tid == 0) reinterpret_cast<unsigned long long*>(a.fin.x_all)[4096 + 2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
@@ -1854,27 +1906,82 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   } else {
     // up2 ConvBlock (relu(acc + bias)) -> final Conv1D 1x1 128 -> n_out (networks.py:1074)
     // -> p_sample epilogue; one thread per output row.
+    // Staged (unfused final level): the C tile goes to LDS as sample-major rows, then each row thread
+    // runs relu(row + maps) . wf over the 128 channels.  TF (fused final level, transposed
+    // accumulators): lane lr of wave (wm, wn) holds tile rows wm * 96 + 32 i + lr and, per jn, the 16
+    // channels wn * 64 + jn * 32 + 8 g + 4 h + q (register 4 g + q); it adds the map rows, applies the
+    // relu and dots its 32 channels with wf4 in registers -- no C-tile staging -- and the four
+    // (wn, h) partial sums of a row meet in LDS [4][MT][4].
     float* fin = reinterpret_cast<float*>(smem);
-    float* wfl = fin + G::MT * G::FIN_LD;
-    float* xst = wfl + 128 * 4;                       // [MT][2] x_next of this tile's rows
+    // TF: the partials [4][MT][4] and, after the row loop, the fused down0's map rows [48][128] share fin
+    static_assert(!TF || 4 * G::MT * 4 <= 48 * 128, "TF partials inside the down0 map region");
+    float* wfl = fin + (TF ? 48 * 128 : G::MT * G::FIN_LD);
+    float* xst = wfl + (TF ? 0 : 128 * 4);            // [MT][2] x_next of this tile's rows
     const FinalArgs& f = a.fin;
     const int n_out = f.n_out;
     const bool fuse_next = f.next.t_uniform >= 0 && f.x_next != nullptr;
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
+    if constexpr (TF) {
+      static_assert(!TF || (G::WM == 2 && G::WN == 2 && G::FUSED && G::PHROWS == 96), "TF: one phase per wave row");
+      f32x4 wq[2][4][4];                              // wf4 rows of this lane's 32 channels
 #pragma unroll
       for (int jn = 0; jn < 2; ++jn)
 #pragma unroll
-        for (int rg = 0; rg < 16; ++rg) {
-          const int r = wm * 96 + i * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * h;
-          int sr, lr_;
-          G::row_sl(r, sr, lr_);
-          fin[(sr * L + lr_) * G::FIN_LD + wn * 64 + jn * 32 + lr] = acc[i][jn][rg];
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            wq[jn][g][q] = *reinterpret_cast<const f32x4*>(f.wf4 + (wn * 64 + jn * 32 + 8 * g + 4 * h + q) * 4);
+      const float* fm = reinterpret_cast<const float*>(smem + G::FMAP_OFF);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int r = wm * 96 + 32 * i + lr;          // tile row [phase][m][sample]
+        int sr, lr_;
+        G::row_sl(r, sr, lr_);
+        const int br = min(m0 + sr, B - 1);           // absent samples: finite values, never stored
+        const float *mt, *mc;
+        if (fin_fast) {                               // the tile's map rows, prefetched into LDS
+          mt = fm + lr_ * G::FIN_LD;
+          mc = mt + G::FMAP_STRIDE * 4;
+        } else {                                      // per-sample t / condition: the rows from L2
+          const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[br];
+          const int tac = a.tac ? a.tac[br] : 0;
+          mt = a.tmap + ((size_t)t * L + lr_) * cout;
+          mc = a.cmap + ((size_t)tac * L + lr_) * cout;
         }
-    // final kernel as [n][4] (zero-padded when n_out == 2) for float4 reads
-    for (int e = tid; e < 128 * 4; e += kThreads) {
-      const int nn = e >> 2, o = e & 3;
-      wfl[e] = o < n_out ? f.wf[nn * n_out + o] : 0.f;
+        f32x4 o4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int n = wn * 64 + jn * 32 + 8 * g + 4 * h;
+            const f32x4 hv = *reinterpret_cast<const f32x4*>(mt + n) + *reinterpret_cast<const f32x4*>(mc + n);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float hq = fmaxf(acc[i][jn][4 * g + q] + hv[q], 0.f);
+              o4[0] = fmaf(hq, wq[jn][g][q][0], o4[0]);
+              o4[1] = fmaf(hq, wq[jn][g][q][1], o4[1]);
+              o4[2] = fmaf(hq, wq[jn][g][q][2], o4[2]);
+              o4[3] = fmaf(hq, wq[jn][g][q][3], o4[3]);
+            }
+          }
+        *reinterpret_cast<f32x4*>(fin + ((wn * 2 + h) * G::MT + r) * 4) = o4;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+          for (int rg = 0; rg < 16; ++rg) {
+            const int r = wm * 96 + i * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * h;
+            int sr, lr_;
+            G::row_sl(r, sr, lr_);
+            fin[(sr * L + lr_) * G::FIN_LD + wn * 64 + jn * 32 + lr] = acc[i][jn][rg];
+          }
+      // final kernel as [n][4] (zero-padded when n_out == 2) for float4 reads
+      for (int e = tid; e < 128 * 4; e += kThreads) {
+        const int nn = e >> 2, o = e & 3;
+        wfl[e] = o < n_out ? f.wf[nn * n_out + o] : 0.f;
+      }
     }
     // Fused next-step down0: its weights and (single-condition) map rows are loaded into
     // registers here so their latency hides behind the row loop below.
@@ -1916,7 +2023,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       const float* mp = a.tmap ? a.tmap + ((size_t)t * L + l) * cout : nullptr;
       const float* cp = a.cmap ? a.cmap + ((size_t)tac * L + l) * cout : nullptr;
       f32x4 o4 = {0.f, 0.f, 0.f, 0.f};
-      auto dot = [&](const float* mq, const float* cq) {
+      [[maybe_unused]] auto dot = [&](const float* mq, const float* cq) {
 #pragma unroll 4
         for (int n = 0; n < 128; n += 4) {
           f32x4 hv = *reinterpret_cast<const f32x4*>(fin + r * G::FIN_LD + n);
@@ -1933,9 +2040,18 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
           }
         }
       };
-      const bool fin_lds = G::FIN_MAPS && fin_fast;   // the same map rows, prefetched into LDS
-      const float* lm = reinterpret_cast<const float*>(smem + G::FMAP_OFF) + l * G::FIN_LD;
-      dot(fin_lds ? lm : mp, fin_lds ? lm + G::FMAP_STRIDE * 4 : cp);
+      if constexpr (TF) {                            // the row's four (wn, h) partial sums
+        const int rt = (l & 1) * G::PHROWS + (l >> 1) * G::S + s_me;
+        const f32x4 p0 = *reinterpret_cast<const f32x4*>(fin + (0 * G::MT + rt) * 4);
+        const f32x4 p1 = *reinterpret_cast<const f32x4*>(fin + (1 * G::MT + rt) * 4);
+        const f32x4 p2 = *reinterpret_cast<const f32x4*>(fin + (2 * G::MT + rt) * 4);
+        const f32x4 p3 = *reinterpret_cast<const f32x4*>(fin + (3 * G::MT + rt) * 4);
+        o4 = (p0 + p1) + (p2 + p3);
+      } else {
+        const bool fin_lds = G::FIN_MAPS && fin_fast;   // the same map rows, prefetched into LDS
+        const float* lm = reinterpret_cast<const float*>(smem + G::FMAP_OFF) + l * G::FIN_LD;
+        dot(fin_lds ? lm : mp, fin_lds ? lm + G::FMAP_STRIDE * 4 : cp);
+      }
       float o[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) o[q] = o4[q] + bfin[q];
@@ -2282,6 +2398,9 @@ static hipError_t launch_conv_xs(int kind, const ConvArgs<T>& a, hipStream_t s) 
       case LK_UP0_F: return launch_one<T, LK_UP0_F, XS>(a, s);
       case LK_UP1_F: return launch_one<T, LK_UP1_F, XS>(a, s);
       case LK_UP2_F: return launch_one<T, LK_UP2_F, XS>(a, s);
+      case LK_UP2_FX3:
+        if constexpr (XS != 0) return launch_one<T, LK_UP2_FX3, XS>(a, s);
+        break;
     }
   }
   return hipErrorInvalidValue;
@@ -2313,8 +2432,10 @@ hipError_t launch_down0(const Down0Args& a, hipStream_t s, bool x3) {
 }
 
 template hipError_t launch_conv<bf16>(int, const ConvArgs<bf16>&, hipStream_t, bool);
+#if !CONV_DOWN1_CORES   // (the co-residency experiment's 32-B down1 chunks exist for the 16-bit MFMA path only)
 template hipError_t launch_conv<f16>(int, const ConvArgs<f16>&, hipStream_t, bool);
 template hipError_t launch_conv<float>(int, const ConvArgs<float>&, hipStream_t, bool);
+#endif
 hipError_t launch_set_rng(unsigned long long* dst, unsigned long long seed, unsigned long long off, hipStream_t s) {
   hipLaunchKernelGGL(set_rng_kernel, dim3(1), dim3(64), 0, s, dst, seed, off);
   return hipGetLastError();

@@ -4,7 +4,7 @@
 #            build, compared array by array (bf16 / fp16 / bf16x3 forwards + 20-step loops)
 #   tests    the GPU test suite;  smoke  __graft_entry__.smoke()
 #   bench    the driver's bench command (1 GPU) and a rocprofv3 kernel-stats pass
-#   ab       REPS interleaved bench pairs: this build vs each ALT (BENCH_EXTRA: more bench flags)
+#   ab       REPS interleaved bench pairs: this build vs each ALT build and each ALTENVS setting (VAR=value)
 # Usage: ALTS="pre_prune.so" STAGES="bitwise tests" bash scripts/gpu_r4.sh TAG
 set -o pipefail
 TAG=${1:-r4}
@@ -48,6 +48,9 @@ if has ab; then
       timeout -k 10 300 python bench.py --steps 3 --no-cpu-baseline --no-extras --dtype $d > $OUT/ab_cur_${d}_$rep.json 2>/dev/null || exit 1
       for alt in $ALTS; do
         PETDIFF_LIB=$GRAFT_REPO_ROOT/scripts/micro/alt/$alt timeout -k 10 300 python bench.py --steps 3 --no-cpu-baseline --no-extras --dtype $d > $OUT/ab_${alt%.so}_${d}_$rep.json 2>/dev/null || exit 1
+      done
+      for ev in $ALTENVS; do
+        env $ev timeout -k 10 300 python bench.py --steps 3 --no-cpu-baseline --no-extras --dtype $d > $OUT/ab_env_${ev//[=]/_}_${d}_$rep.json 2>/dev/null || exit 1
       done
     done
   done

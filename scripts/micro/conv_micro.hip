@@ -7,6 +7,7 @@
 #include <vector>
 #include <algorithm>
 #include <string>
+#include <cstring>
 
 using namespace petdiff;
 
@@ -153,6 +154,19 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
            cyc[nb / 2] / nmfma, clk[nb / 2], clk[0], clk[nb - 1]);
   }
 #endif
+  {   // output checksum (variants of one layer must agree to rounding)
+    const size_t n = std::min<size_t>(rows_out * cout, 1 << 20);
+    std::vector<unsigned short> hb(n);
+    CK(hipMemcpy(hb.data(), out, n * 2, hipMemcpyDeviceToHost));
+    double cs = 0.0;
+    for (size_t i = 0; i < n; ++i) {
+      unsigned u = (unsigned)hb[i] << 16;
+      float f;
+      memcpy(&f, &u, 4);
+      cs += f;
+    }
+    printf("   checksum %.6e over %zu outputs, LDS %d B per workgroup, %d threads\n", cs, n, G::SMEM, G::NTH);
+  }
   const double flop = G::FUSED ? 2.0 * rows_out * cout * ((double)c1 * G::TAPS + (double)c2 * G::TAPS2)
                                : 2.0 * rows_out * cout * (double)(c1 + c2) * G::TAPS;
   printf("%-12s mode %d  %8.2f us  %7.1f TF/s (executed)  grid %d\n", name, CONV_EXP_MODE, us, flop / us * 1e-6,
@@ -168,6 +182,10 @@ int main(int argc, char** argv) {
   const char* only = argc > 2 ? argv[2] : "";
   if (std::string(only) == "u2") {   // the final level alone
     run<LK_UP2_F>("up2.fused", B, 128, 256, 128, it);
+    return 0;
+  }
+  if (std::string(only) == "d1") {   // down1 alone (co-residency experiment: B = 1024 and 2048)
+    run<LK_DOWN1>("down1", B, 128, 0, 256, it);
     return 0;
   }
   if (std::string(only) == "u0") {   // the dominant level alone
