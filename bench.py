@@ -72,7 +72,7 @@ STEP_KERNELS = (
      12 * 2 * 1074 * 512 + 12 * 7 * 1024 * 512, UP0_FUSED_EXEC_FLOP_PER_SAMPLE // 2),
     ('up1.block', 'conv_kernel<up1 fused> (UpSampling1D + k2 562->256 + ConvBlock 512->256 k6+res, L=24)',
      24 * 2 * 562 * 256 + 24 * 7 * 512 * 256, 24 * 6 * 256 * 256 + 24 * 4 * 512 * 256 + 2 * 512 * 256),
-    ('up2.block', 'conv_kernel<up2 fused> (UpSampling1D + k2 306->128 + ConvBlock 256->128 k6+res, L=48) + final '
+    ('up2.block+final+p_sample', 'conv_kernel<up2 fused> (UpSampling1D + k2 306->128 + ConvBlock 256->128 k6+res, L=48) + final '
                   '1x1 128->4 + p_sample + next-step down0 (52->128 k6+res)',
      48 * 2 * 306 * 128 + 48 * 7 * 256 * 128 + 48 * 128 * 4 + 48 * 7 * 52 * 128,
      48 * 6 * 128 * 128 + 48 * 4 * 256 * 128 + 2 * 256 * 128),
@@ -87,8 +87,8 @@ def step_kernel_bytes(key, dtype):
     acts = {'down1': 24 * 128 + 24 * 256 + 12 * 256, 'down2': 12 * 256 + 12 * 512 + 6 * 512,
             'down3': 6 * 512 + 6 * 1024, 'up0.block': 12 * 512 + 6 * 1024 + 12 * 512,
             'up1.block': 24 * 256 + 12 * 512 + 24 * 256,
-            'up2.block': 48 * 128 + 24 * 256 + 48 * 128 + 24 * 128}[key]   # up2: + next s0 / p0
-    return acts * e + (2 * 96 * 4 if key == 'up2.block' else 0)
+            'up2.block+final+p_sample': 48 * 128 + 24 * 256 + 48 * 128 + 24 * 128}[key]   # up2: + next s0 / p0
+    return acts * e + (2 * 96 * 4 if key.startswith('up2') else 0)
 
 
 def weight_bytes(key, dtype):
@@ -96,9 +96,14 @@ def weight_bytes(key, dtype):
     e = 4 if dtype in ('bf16x3', 'float32') else 2
     w = {'down1': 6 * 128 * 256, 'down2': 6 * 256 * 512, 'down3': 6 * 512 * 1024,
          'up0.block': 6 * 512 * 512 + 8 * 1024 * 512, 'up1.block': 6 * 256 * 256 + 8 * 512 * 256,
-         'up2.block': 6 * 128 * 128 + 8 * 256 * 128}[key]
+         'up2.block+final+p_sample': 6 * 128 * 128 + 8 * 256 * 128}[key]
     return w * e
 
+
+# per-layer timing: every timed launch runs TIMING_REPS times back to back between its two HIP events
+# (ImprovedDDPM.set_kernel_timing), so one event's queue gap is shared by 8 launches and the mean launch
+# time tracks rocprofv3's kernel duration
+TIMING_REPS = 8
 
 # training step: forward + data grad + weight grad of every layer, incl. the
 # per-sample condition encoder / label projections / time MLP (6,002,304 FLOP per sample forward)
@@ -275,7 +280,8 @@ def pmc_fields(pmc, avg_s):
 
 def up0_roofline(layer_ms, bt, dtype, tflops_pipeline=None):
     """`roofline` of the dominant kernel (up0's fused level; up0.block when unfused) from per-layer HIP-event
-    timing (ms, count) of one eager generate at bt samples per launch: algorithmic FLOP per launch / mean
+    timing (ms, count) of one eager generate at bt samples per launch (each launch repeated TIMING_REPS times
+    between its events): algorithmic FLOP per launch / mean
     launch time against the dtype's dense MFMA peak (fp16 dense = bf16 dense; bf16x3 runs 3 bf16 products
     per fp32 product, so its peak is bf16 dense / 3; f32: the fp32 MFMA peak), plus the PMC fields of the
     same kernel and dtype when the committed counters were taken on this build (load_pmc)."""
@@ -347,11 +353,11 @@ def kernel_table(layer_ms, bt, dtype):
         avg = ms / cnt / 1e3
         alg = 2 * alg_mac * bt
         ab = (step_kernel_bytes(key, dtype)) * bt + weight_bytes(key, dtype)
-        r = {'kernel': name, 'timing_key': key, 'launches_per_generate': cnt, 'us': round(avg * 1e6, 2),
+        r = {'kernel': name, 'timing_key': key, 'launches_per_generate': cnt // TIMING_REPS, 'us': round(avg * 1e6, 2),
              'alg_gflop': round(alg / 1e9, 3), 'alg_over_peak': round(alg / avg / 1e12 / peak, 4),
              'exec_frac': round(xm * 2 * exe_mac * bt / avg / 1e12 / PEAK_BF16_TFLOPS, 4), 'alg_bytes': int(ab)}
         if pk is not None:
-            c = pk['per_launch'].get(key.replace('.block', '.fused'), {})
+            c = pk['per_launch'].get(key.split('+')[0].replace('.block', '.fused'), {})
             if c.get('bytes'):
                 r['traffic'] = int(c['bytes'])
                 r['traffic_ratio'] = round(c['bytes'] / ab, 2)
@@ -605,7 +611,7 @@ def bf16x3_rate(cond, B, n_rev, dev):
     tf = FLOP_PER_SAMPLE_STEP * n_rev * B / el / 1e12
     te = 3 * EXEC_MFMA_FLOP_PER_SAMPLE_STEP_FUSED * n_rev * B / el / 1e12
     # the dominant kernel of THIS network: per-layer HIP events over one eager generate on the launch stream
-    m.set_kernel_timing(True)
+    m.set_kernel_timing(True, reps=TIMING_REPS)
     m.ddpm_loop(x, cond[None], num_timesteps=n_rev, seed=2, use_graph=False)
     lm = m.get_kernel_timing()
     m.set_kernel_timing(False)
@@ -790,7 +796,7 @@ def main():
     # per-layer kernel timing (HIP events on the launch stream, one eager generate)
     layer_ms = None
     if not args.no_kernel_timing:
-        model.set_kernel_timing(True)
+        model.set_kernel_timing(True, reps=TIMING_REPS)
         bt = min(B, chunk)   # one launch's worth of samples
         model.ddpm_loop(x_T[:bt], cond, num_timesteps=n_rev, seed=2, sample_offset=offset, use_graph=False,
                         tac=tac[:bt] if n_tac > 1 else None)

@@ -195,10 +195,14 @@ int petdiff_get_activation(petdiff_handle h, int level, float* out_dev, int B, v
 
 /* Per-layer kernel timing with HIP events on the launch stream (eager mode
  * only).  layer ids: 0 down0, 1..9 = down1, down2, down3, up0.conv2, up0.block,
- * up1.conv2, up1.block, up2.conv2, up2.block(+final+p_sample). */
+ * up1.conv2, up1.block, up2.conv2, up2.block(+final+p_sample).
+ * enable: 0 off; n >= 1 on, each timed layer launch repeated n times back to back
+ * (at most 64; the kernels are idempotent) so the event pair's queue gap is shared
+ * by n launches. */
 #define PETDIFF_NUM_LAYERS 10
 int petdiff_set_timing(petdiff_handle h, int enable);
-/* Synchronises; fills total ms and launch count per layer, then resets. */
+/* Synchronises; fills total ms and launch count (timed launches, repeats included)
+ * per layer, then resets. */
 int petdiff_get_timing(petdiff_handle h, float* total_ms, int* count);
 
 const char* petdiff_last_error(void);

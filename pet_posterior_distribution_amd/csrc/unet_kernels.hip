@@ -26,10 +26,11 @@
 #ifndef CONV_LOADERS
 #define CONV_LOADERS 1
 #endif
-// The fused final level's time / label map rows: 1 = staged in LDS by LDS-DMA at kernel start, 0 = read
-// from L2 in the epilogue (A/B switch)
+// The fused final level's time / label map rows: 0 = read from L2 by the transposed final conv in the
+// epilogue, 1 = staged in LDS by LDS-DMA at kernel start (54 KB in the start-up burst of all 256
+// workgroups; A/B: 5035-5051 vs 5093 samples/s for 0, profiles/r04/ab_r4d)
 #ifndef CONV_FIN_LDS_MAPS
-#define CONV_FIN_LDS_MAPS 1
+#define CONV_FIN_LDS_MAPS 0
 #endif
 
 // Diagnostic builds only (scripts/micro/conv_micro.hip): bit 1 drops the K-loop DMA,
@@ -1597,6 +1598,10 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     prefetch_maps();
     wait_vmcnt<0>();
     __syncthreads();
+#if CONV_EXP_MODE & 128
+    st_c0 = __builtin_amdgcn_s_memtime();
+    st_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
     for (int kc = 0; kc + 1 < NC; ++kc) {
       compute(smem + (kc & 1) * G::STAGE, Yes{}, kc + 1, (kc + 1) & 1, Seg1{}, 0, P0{});
       wait_vmcnt<0>();
@@ -1718,7 +1723,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     mfma_bf16(1);   // the last chunk's last step (NS even)
   }
 #if CONV_EXP_MODE & 128
-  if constexpr (G::STAGES == 3) {   // diagnostic: main-loop cycles and the clock (s_memrealtime = 100 MHz)
+  {   // diagnostic: main-loop cycles and the clock (s_memrealtime = 100 MHz)
     const unsigned long long st_c1 = __builtin_amdgcn_s_memtime(), st_r1 = __builtin_amdgcn_s_memrealtime();
     if (tid == 0) {
       unsigned long long* dbg = reinterpret_cast<unsigned long long*>(a.fin.x_all);
@@ -1727,6 +1732,9 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       dbg[8192 + 4 * blockIdx.x] = st_rin;
       dbg[8192 + 4 * blockIdx.x + 1] = st_r0;
       dbg[8192 + 4 * blockIdx.x + 2] = st_r1;
+      // where the workgroup ran: HW_ID (cu_id [11:8], sh_id [12], se_id [15:13]) and XCC_ID (hwreg 20)
+      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4), xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+      dbg[16384 + blockIdx.x] = ((unsigned long long)(xcc & 15) << 16) | ((hw >> 8) & 0xff);
     }
   }
 #endif
@@ -1984,7 +1992,8 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       }
     }
     // Fused next-step down0: its weights and (single-condition) map rows are loaded into
-    // registers here so their latency hides behind the row loop below.
+    // registers here so their latency hides behind the row loop below (issued before the TF final
+    // conv instead they measured slower: up2 39.7 vs 38.5-38.8 us, profiles/r04/ab_r4d/ab_tf_early_*).
     static_assert(G::MT % L == 0 && L == 48, "fused down0 needs whole 48-ROI samples");
     static_assert(G::NTH == kThreads, "fused down0 strides assume one 256-thread block");
     const Down0Args& nd = f.next;

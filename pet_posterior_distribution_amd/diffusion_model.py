@@ -630,8 +630,10 @@ class ImprovedDDPM:
         return stats
 
     # ---------------------------------------------------------- timing
-    def set_kernel_timing(self, enable=True):
-        _lib.check(_lib.lib().petdiff_set_timing(self._ensure_handle(), int(enable)))
+    def set_kernel_timing(self, enable=True, reps=1):
+        """Per-layer HIP-event timing of eager launches; reps > 1 repeats every timed launch back to
+        back (the kernels are idempotent), so the events' queue gap is amortised over reps launches."""
+        _lib.check(_lib.lib().petdiff_set_timing(self._ensure_handle(), int(reps) if enable else 0))
 
     def get_kernel_timing(self):
         ms = (C.c_float * _lib.NUM_LAYERS)()

@@ -3,6 +3,8 @@
 #   bitwise  scripts/lib_bitwise.py dumps of every ALT build (scripts/micro/alt/<name>.so) and of this
 #            build, compared array by array (bf16 / fp16 / bf16x3 forwards + 20-step loops)
 #   tests    the GPU test suite;  smoke  __graft_entry__.smoke()
+#   pmc      rocprofv3 PMC passes (bf16, bf16x3) -> $OUT/pmc_traffic.json (bench.py's per-kernel counters)
+#   cores    scripts/micro/coresident.sh (down1 co-residency experiment, prebuilt binaries)
 #   bench    the driver's bench command (1 GPU) and a rocprofv3 kernel-stats pass
 #   ab       REPS interleaved bench pairs: this build vs each ALT build and each ALTENVS setting (VAR=value)
 # Usage: ALTS="pre_prune.so" STAGES="bitwise tests" bash scripts/gpu_r4.sh TAG
@@ -35,6 +37,19 @@ fi
 if has smoke; then
   timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; exit 1; }
   tail -1 $OUT/smoke.log
+fi
+if has cores; then
+  timeout -k 10 300 bash scripts/micro/coresident.sh > $OUT/coresident.txt 2>&1 || { echo "coresident failed"; tail $OUT/coresident.txt; exit 1; }
+  grep -E "==|down1|checksum" $OUT/coresident.txt | head -40
+fi
+if has pmc; then
+  # PMC passes over the bf16 and bf16x3 networks; the summaries stamp profiles/pmc_traffic.json with this
+  # build's kernel code hash (copied back under gpurun_out/TAG)
+  bash scripts/gpu_pmc.sh ${TAG}_pmc || exit 1
+  python scripts/pmc_summary.py gpurun_out/${TAG}_pmc gpurun_out/${TAG}_pmc/pmc.json --traffic > gpurun_out/${TAG}_pmc/summary.txt 2>&1 || exit 1
+  BENCH_EXTRA="--dtype bf16x3" bash scripts/gpu_pmc.sh ${TAG}_pmc_x3 || exit 1
+  python scripts/pmc_summary.py gpurun_out/${TAG}_pmc_x3 gpurun_out/${TAG}_pmc_x3/pmc.json --traffic --dtype=bf16x3 > gpurun_out/${TAG}_pmc_x3/summary.txt 2>&1 || exit 1
+  cp profiles/pmc_traffic.json $OUT/pmc_traffic.json
 fi
 if has bench; then
   timeout -k 10 500 python bench.py --gpus 1 --steps 20 --warmup 5 ${BENCH_EXTRA} > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail $OUT/bench.err; exit 1; }

@@ -150,6 +150,35 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
            mx(st), med(pro), mx(pro), med(lp), mx(lp), med(epi), mx(epi), (tmax - tmin) * 0.01);
     printf("   epilogue us: acc->LDS+barrier %.2f | read/add/store issue %.2f | store drain %.2f\n", med(ea), med(eb),
            med(ec));
+    {   // co-residency: workgroups whose [start, end] overlap on one CU (HW_ID cu/sh/se + XCC_ID)
+      std::vector<unsigned long long> loc(nb);
+      CK(hipMemcpy(loc.data(), dbg + 16384, nb * 8, hipMemcpyDeviceToHost));
+      std::vector<std::pair<unsigned long long, int>> ev;
+      std::vector<std::pair<unsigned long long, std::pair<unsigned long long, unsigned long long>>> iv;
+      for (int b = 0; b < nb; ++b) iv.push_back({loc[b], {t4[4 * b], t4[4 * b + 3]}});
+      std::sort(iv.begin(), iv.end());
+      int maxc = 0, ncu = 0;
+      double ovl = 0.0, busy = 0.0;
+      for (size_t i = 0; i < iv.size();) {
+        size_t j = i;
+        while (j < iv.size() && iv[j].first == iv[i].first) ++j;
+        ++ncu;
+        std::vector<std::pair<unsigned long long, int>> e;
+        for (size_t k = i; k < j; ++k) { e.push_back({iv[k].second.first, 1}); e.push_back({iv[k].second.second, -1}); }
+        std::sort(e.begin(), e.end());
+        int c = 0;
+        for (size_t k = 0; k + 1 < e.size(); ++k) {
+          c += e[k].second;
+          maxc = std::max(maxc, c);
+          const double d = (e[k + 1].first - e[k].first) * 0.01;
+          if (c >= 1) busy += d;
+          if (c >= 2) ovl += d;
+        }
+        i = j;
+      }
+      printf("   co-residency: %d CUs used, max %d workgroups at once on a CU, %.1f %% of CU-busy time with >= 2\n", ncu, maxc,
+             busy > 0 ? 100.0 * ovl / busy : 0.0);
+    }
     printf("   loop cycles median %.0f (%.1f per MFMA), clock median %.3f GHz [%.3f..%.3f]\n", cyc[nb / 2],
            cyc[nb / 2] / nmfma, clk[nb / 2], clk[0], clk[nb - 1]);
   }

@@ -459,18 +459,18 @@ def test_bench_step_kernel_table(monkeypatch):
     tot = sum(k[2] for k in bench.STEP_KERNELS) + 48 * 7 * 52 * 128 * 0
     # App. A total (148.18 M MAC) = down0 + the 6 kernels' counts (up2's includes the next step's down0)
     assert tot == bench.FLOP_PER_SAMPLE_STEP // 2
+    from pet_posterior_distribution_amd import _lib as L
     us = {'down0': 0, 'down1': 13.4, 'down2': 18.3, 'down3': 25.6, 'up0.block': 59.7, 'up1.block': 37.6,
-          'up2.block': 40.1}
-    lm = {k: (0.0, 0) for k in ('down0', 'down1', 'down2', 'down3', 'up0.conv2', 'up0.block', 'up1.conv2',
-                                 'up1.block', 'up2.conv2', 'up2.block')}
+          'up2.block+final+p_sample': 40.1}
+    lm = {k: (0.0, 0) for k in L.LAYER_NAMES}           # the keys ImprovedDDPM.get_kernel_timing returns
     for k, u in us.items():
-        lm[k] = (u * 1e-3 * 1000, 1000 if u else 0)
+        lm[k] = (u * 1e-3 * 1000 * bench.TIMING_REPS, 1000 * bench.TIMING_REPS if u else 0)
     monkeypatch.setattr(_lib, 'kernel_code_hash', lambda *a, **k: 'no such build')
     lm3 = {k: (v[0] * 2.6, v[1]) for k, v in lm.items()}     # bf16x3 runs about 2.6 x the bf16 times
     for dt, lmd in (('bfloat16', lm), ('bf16x3', lm3)):
         kt = bench.kernel_table(lmd, 1024, dt)
         assert [r['timing_key'] for r in kt['kernels']] == ['down1', 'down2', 'down3', 'up0.block', 'up1.block',
-                                                              'up2.block']
+                                                              'up2.block+final+p_sample']
         assert kt['pmc'] is None and all('mfma_util' not in r for r in kt['kernels'])
         for r in kt['kernels']:
             assert 0 < r['exec_frac'] < 1 and r['alg_bytes'] > 0
