@@ -3,6 +3,7 @@
 #   bitwise  scripts/lib_bitwise.py dumps of every ALT build (scripts/micro/alt/<name>.so) and of this
 #            build, compared array by array (bf16 / fp16 / bf16x3 forwards + 20-step loops)
 #   tests    the GPU test suite;  smoke  __graft_entry__.smoke()
+#   micro    conv_micro step layers in isolation + stamps (prebuilt binaries)
 #   pmc      rocprofv3 PMC passes (bf16, bf16x3) -> $OUT/pmc_traffic.json (bench.py's per-kernel counters)
 #   cores    scripts/micro/coresident.sh (down1 co-residency experiment, prebuilt binaries)
 #   bench    the driver's bench command (1 GPU) and a rocprofv3 kernel-stats pass
@@ -41,6 +42,12 @@ fi
 if has cores; then
   timeout -k 10 300 bash scripts/micro/coresident.sh > $OUT/coresident.txt 2>&1 || { echo "coresident failed"; tail $OUT/coresident.txt; exit 1; }
   grep -E "==|down1|checksum" $OUT/coresident.txt | head -40
+fi
+if has micro; then
+  # conv_micro (prebuilt: MODES="0 128" bash scripts/micro/build.sh): the 16-bit step layers in isolation, with
+  # per-workgroup s_memrealtime stamps in mode 128 (prologue / loop / epilogue; the final level's epilogue parts)
+  (cd scripts/micro && timeout -k 10 120 ./conv_micro_m0 1024 f && timeout -k 10 120 ./conv_micro_m128 1024 f) > $OUT/micro.txt 2>&1 || { echo "micro failed"; tail $OUT/micro.txt; exit 1; }
+  grep -E "us|mode" $OUT/micro.txt | head -40
 fi
 if has pmc; then
   # PMC passes over the bf16 and bf16x3 networks; the summaries stamp profiles/pmc_traffic.json with this

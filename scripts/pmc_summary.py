@@ -12,7 +12,7 @@ from collections import defaultdict
 
 
 LAYERS = ['down1', 'down2', 'down3', 'up0.conv2', 'up0.block', 'up1.conv2', 'up1.block', 'up2.conv2', 'up2.block',
-          'up0.fused', 'up1.fused', 'up2.fused']
+          'up0.fused', 'up1.fused', 'up2.fused', 'up2.fused']   # kind 12: the bf16x3 final level (LK_UP2_FX3)
 
 
 def short(name):
