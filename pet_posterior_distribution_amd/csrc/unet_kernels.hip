@@ -2383,6 +2383,8 @@ static hipError_t launch_one(const ConvArgs<T>& a, hipStream_t s) {
   if (a.B <= 0) return hipSuccess;
   if (a.cout % G::NT != 0 || a.c1 % G::KC != 0 || a.c2 % G::KC != 0) return hipErrorInvalidValue;
   if (G::FUSED && (!a.src2 || !a.epack || a.c2 <= 0)) return hipErrorInvalidValue;
+  // the fused final level's transposed epilogue reads the packed final kernel and both map tables
+  if (G::FIN_MAPS && (!a.fin.wf4 || !a.tmap || !a.cmap)) return hipErrorInvalidValue;
   const int nM = (a.B + G::S - 1) / G::S;
   const int total = nM * (a.cout / G::NT);
   hipLaunchKernelGGL((conv_kernel<T, KIND, XS>), dim3(total), dim3(G::NTH), 0, s, a);

@@ -46,7 +46,8 @@ fi
 if has micro; then
   # conv_micro (prebuilt: MODES="0 128" bash scripts/micro/build.sh): the 16-bit step layers in isolation, with
   # per-workgroup s_memrealtime stamps in mode 128 (prologue / loop / epilogue; the final level's epilogue parts)
-  (cd scripts/micro && timeout -k 10 120 ./conv_micro_m0 1024 f && timeout -k 10 120 ./conv_micro_m128 1024 f) > $OUT/micro.txt 2>&1 || { echo "micro failed"; tail $OUT/micro.txt; exit 1; }
+  (cd scripts/micro && timeout -k 10 120 ./conv_micro_m0 1024 f && timeout -k 10 120 ./conv_micro_m128 1024 f && \
+   timeout -k 10 120 ./conv_micro_m0 1024 x && timeout -k 10 120 ./conv_micro_m128 1024 x) > $OUT/micro.txt 2>&1 || { echo "micro failed"; tail $OUT/micro.txt; exit 1; }
   grep -E "us|mode" $OUT/micro.txt | head -40
 fi
 if has pmc; then

@@ -28,17 +28,20 @@ __global__ void fill_f32(float* p, size_t n, unsigned seed) {
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
-template <int KIND>
+// XS = 1: the bf16x3 instance ([hi | lo] activation rows; paired chunks on the 64-B-row layers, 2 x the
+// bf16 chunks, three passes on the 32-B final level, 3 x)
+template <int KIND, int XS = 0>
 void run(const char* name, int B, int c1, int c2, int cout, int iters) {
   using G = ConvGeom<bf16, KIND>;
+  constexpr int RS = XS ? 2 : 1, XM = XS ? (x3_paired(KIND) ? 2 : 3) : 1;
   const size_t rows_in = (size_t)B * G::LIN, rows_out = (size_t)B * G::L;
-  const int NC = c1 / G::KC + c2 / G::KC;
+  const int NC = XM * (c1 / G::KC + c2 / G::KC);
   bf16 *s1, *s2 = nullptr, *w, *out, *pool;
   float *cmap, *tmap, *bias;
-  CK(hipMalloc(&s1, rows_in * c1 * 2));
+  CK(hipMalloc(&s1, rows_in * c1 * 2 * RS));
   const size_t rows_in2 = G::FUSED ? (size_t)B * G::LH : rows_in;   // fused: src2 = the coarse input b
-  if (c2) CK(hipMalloc(&s2, rows_in2 * c2 * 2));
-  const int n1 = c1 / G::KC, n2 = c2 / G::KC;
+  if (c2) CK(hipMalloc(&s2, rows_in2 * c2 * 2 * RS));
+  const int n1 = XM * (c1 / G::KC), n2 = XM * (c2 / G::KC);
   const size_t wbytes = G::FUSED ? (size_t)(cout / G::NT) * (n1 * G::B_BYTES + n2 * G::B2_BYTES)
                                  : (size_t)(cout / G::NT) * NC * G::B_BYTES;
   bf16* ep = nullptr;
@@ -46,13 +49,13 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
   CK(hipMalloc(&ep, ebytes));
   fill_bf16<<<1024, 256>>>(ep, ebytes / 2, 11);
   CK(hipMalloc(&w, wbytes));
-  CK(hipMalloc(&out, rows_out * cout * 2));
-  CK(hipMalloc(&pool, rows_out * cout));
+  CK(hipMalloc(&out, rows_out * cout * 2 * RS));
+  CK(hipMalloc(&pool, rows_out * cout * RS));
   CK(hipMalloc(&cmap, (size_t)G::L * cout * 4));
   CK(hipMalloc(&tmap, (size_t)1000 * G::L * cout * 4));
   CK(hipMalloc(&bias, cout * 4));
-  fill_bf16<<<1024, 256>>>(s1, rows_in * c1, 1);
-  if (c2) fill_bf16<<<1024, 256>>>(s2, rows_in2 * c2, 2);
+  fill_bf16<<<1024, 256>>>(s1, rows_in * c1 * RS, 1);
+  if (c2) fill_bf16<<<1024, 256>>>(s2, rows_in2 * c2 * RS, 2);
   fill_bf16<<<1024, 256>>>(w, wbytes / 2, 3);
   fill_f32<<<1024, 256>>>(cmap, (size_t)G::L * cout, 4);
   fill_f32<<<1024, 256>>>(tmap, (size_t)1000 * G::L * cout, 5);
@@ -75,7 +78,7 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
   a.src1 = s1; a.c1 = c1; a.src2 = s2; a.c2 = c2; a.wpack = w; a.out = out; a.out_pool = pool;
   a.cmap = cmap; a.tmap = tmap; a.bias = bias; a.tac = nullptr; a.tvec = nullptr; a.t_uniform = 500;
   a.B = B; a.cout = cout; a.n_t = 1000; a.n_tac = 1;
-  a.fin.wf = wf; a.fin.bf = bfv; a.fin.n_out = 4; a.fin.x_t = xt; a.fin.z = nullptr; a.fin.rng = rng;
+  a.fin.wf = wf; a.fin.wf4 = wf; a.fin.bf = bfv;   // wf: [128][4] (n_out = 4), also the packed wf4 layout a.fin.n_out = 4; a.fin.x_t = xt; a.fin.z = nullptr; a.fin.rng = rng;
   a.fin.rng_step = 3; a.fin.tab = tab; a.fin.T = 1000; a.fin.learn_mode = 2; a.fin.param_mode = 0;
   a.fin.flag_var_tilde = 1; a.fin.x_next = xn;
   a.epack = ep;
@@ -85,8 +88,8 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
   CK(hipMalloc(&w0, 6 * 2 * 128 * 4));
   CK(hipMalloc(&m0c, 48 * 128 * 4));
   CK(hipMalloc(&m0t, (size_t)1000 * 48 * 128 * 4));
-  CK(hipMalloc(&s0n, (size_t)B * 48 * 128 * 2));
-  CK(hipMalloc(&p0n, (size_t)B * 24 * 128 * 2));
+  CK(hipMalloc(&s0n, (size_t)B * 48 * 128 * 2 * RS));
+  CK(hipMalloc(&p0n, (size_t)B * 24 * 128 * 2 * RS));
   fill_f32<<<64, 256>>>(w0, 6 * 2 * 128, 12);
   fill_f32<<<64, 256>>>(m0c, 48 * 128, 13);
   fill_f32<<<1024, 256>>>(m0t, (size_t)1000 * 48 * 128, 14);
@@ -102,12 +105,12 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
   a.fin.x_all = reinterpret_cast<float*>(dbg);
 #endif
   CK(hipDeviceSynchronize());
-  for (int i = 0; i < 20; ++i) CK(launch_conv<bf16>(KIND, a, 0));
+  for (int i = 0; i < 20; ++i) CK(launch_conv<bf16>(KIND, a, 0, XS != 0));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   CK(hipEventRecord(e0, 0));
-  for (int i = 0; i < iters; ++i) CK(launch_conv<bf16>(KIND, a, 0));
+  for (int i = 0; i < iters; ++i) CK(launch_conv<bf16>(KIND, a, 0, XS != 0));
   CK(hipEventRecord(e1, 0));
   CK(hipEventSynchronize(e1));
   float ms;
@@ -122,8 +125,8 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
     for (int b = 0; b < nb; ++b) { cyc.push_back((double)h[2 * b]); clk.push_back(h[2 * b] / (h[2 * b + 1] * 1e-8) * 1e-9); }
     std::sort(cyc.begin(), cyc.end());
     std::sort(clk.begin(), clk.end());
-    const double nmfma = G::FUSED ? ((double)c1 / G::KC * G::TAPS + (double)c2 / G::KC * G::TAPS2) * (G::ROWB / 32) * 6
-                                  : (double)(c1 + c2) / G::KC * G::TAPS * (G::ROWB / 32) * 6;
+    const double nmfma = (XS ? 3 : 1) * (G::FUSED ? ((double)c1 / G::KC * G::TAPS + (double)c2 / G::KC * G::TAPS2) * (G::ROWB / 32) * 6
+                                  : (double)(c1 + c2) / G::KC * G::TAPS * (G::ROWB / 32) * 6);
     std::vector<unsigned long long> t4(4 * nb);
     CK(hipMemcpy(t4.data(), dbg + 8192, 4 * nb * 8, hipMemcpyDeviceToHost));
     unsigned long long tmin = ~0ull, tmax = 0;
@@ -198,7 +201,7 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
   }
   const double flop = G::FUSED ? 2.0 * rows_out * cout * ((double)c1 * G::TAPS + (double)c2 * G::TAPS2)
                                : 2.0 * rows_out * cout * (double)(c1 + c2) * G::TAPS;
-  printf("%-12s mode %d  %8.2f us  %7.1f TF/s (executed)  grid %d\n", name, CONV_EXP_MODE, us, flop / us * 1e-6,
+  printf("%-12s mode %d  %8.2f us  %7.1f TF/s (executed)  grid %d\n", name, CONV_EXP_MODE, us, (XS ? 3 : 1) * flop / us * 1e-6,
          ((B + G::S - 1) / G::S) * (cout / G::NT));
   hipFree(s1); if (s2) hipFree(s2); hipFree(w); hipFree(out); hipFree(pool); hipFree(cmap); hipFree(tmap);
   hipFree(bias); hipFree(wf); hipFree(bfv); hipFree(xt); hipFree(xn); hipFree(tab); hipFree(rng); hipFree(dbg);
@@ -219,6 +222,15 @@ int main(int argc, char** argv) {
   }
   if (std::string(only) == "u0") {   // the dominant level alone
     run<LK_UP0_F>("up0.fused", B, 512, 1024, 512, it);
+    return 0;
+  }
+  if (only[0] == 'x') {   // the bf16x3 step: down layers + fused up levels (the final level's paired instance)
+    run<LK_DOWN1, 1>("down1.x3", B, 128, 0, 256, it);
+    run<LK_DOWN2, 1>("down2.x3", B, 256, 0, 512, it);
+    run<LK_DOWN3, 1>("down3.x3", B, 512, 0, 1024, it);
+    run<LK_UP0_F, 1>("up0.fused.x3", B, 512, 1024, 512, it);
+    run<LK_UP1_F, 1>("up1.fused.x3", B, 256, 512, 256, it);
+    run<LK_UP2_FX3, 1>("up2.fused.x3", B, 128, 256, 128, it);
     return 0;
   }
   if (only[0] == 'f') {   // the product's 16-bit step: down layers + fused up levels
