@@ -2385,6 +2385,13 @@ static hipError_t launch_one(const ConvArgs<T>& a, hipStream_t s) {
   if (G::FUSED && (!a.src2 || !a.epack || a.c2 <= 0)) return hipErrorInvalidValue;
   // the fused final level's transposed epilogue reads the packed final kernel and both map tables
   if (G::FIN_MAPS && (!a.fin.wf4 || !a.tmap || !a.cmap)) return hipErrorInvalidValue;
+  if (G::EPI == EPI_FINAL) {   // every pointer the final epilogue dereferences unconditionally
+    const FinalArgs& f = a.fin;
+    if (!f.wf || !f.bf || f.n_out < 1 || f.n_out > 4) return hipErrorInvalidValue;
+    if (!f.net_out && (!f.x_t || !f.tab || f.T <= 0 || (!f.z && !f.rng))) return hipErrorInvalidValue;
+    if (f.next.t_uniform >= 0 && f.x_next && (!f.next.w0 || !f.next.tmap || !f.next.cmap || !f.next.s0 || !f.next.p0))
+      return hipErrorInvalidValue;
+  }
   const int nM = (a.B + G::S - 1) / G::S;
   const int total = nM * (a.cout / G::NT);
   hipLaunchKernelGGL((conv_kernel<T, KIND, XS>), dim3(total), dim3(G::NTH), 0, s, a);

@@ -78,7 +78,8 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
   a.src1 = s1; a.c1 = c1; a.src2 = s2; a.c2 = c2; a.wpack = w; a.out = out; a.out_pool = pool;
   a.cmap = cmap; a.tmap = tmap; a.bias = bias; a.tac = nullptr; a.tvec = nullptr; a.t_uniform = 500;
   a.B = B; a.cout = cout; a.n_t = 1000; a.n_tac = 1;
-  a.fin.wf = wf; a.fin.wf4 = wf; a.fin.bf = bfv;   // wf: [128][4] (n_out = 4), also the packed wf4 layout a.fin.n_out = 4; a.fin.x_t = xt; a.fin.z = nullptr; a.fin.rng = rng;
+  // wf: [128][4] (n_out = 4), which is also the packed wf4 layout the fused final level reads
+  a.fin.wf = wf; a.fin.wf4 = wf; a.fin.bf = bfv; a.fin.n_out = 4; a.fin.x_t = xt; a.fin.z = nullptr; a.fin.rng = rng;
   a.fin.rng_step = 3; a.fin.tab = tab; a.fin.T = 1000; a.fin.learn_mode = 2; a.fin.param_mode = 0;
   a.fin.flag_var_tilde = 1; a.fin.x_next = xn;
   a.epack = ep;
