@@ -9,7 +9,7 @@ LAYERS = ['down1', 'down2', 'down3', 'up0.conv2', 'up0.block', 'up1.conv2', 'up1
 
 
 def label(name):
-    if 'down0_kernel' in name:
+    if 'down0_kernel' in name or 'down0_mfma_kernel' in name:
         return 'down0'
     # rocprofv3's demangler garbles the bf16 instances of kinds 1 and 2 (down2, down3):
     # conv_kernel<bf16, 1, XS> -> 'conv_kernel<bool _Accum, int, E, XS>',
@@ -34,7 +34,7 @@ def load(path):
 
 
 cols = [load(p) for p in sys.argv[1:]]
-keys = ['down0'] + LAYERS
+keys = ['down0'] + list(dict.fromkeys(LAYERS))
 print('%-10s' % 'kernel' + ''.join('%18s' % ('calls / avg us',) for _ in cols))
 for k in keys:
     print('%-10s' % k + ''.join('%8s %9.2f' % (c[k][0], c[k][1]) if k in c else '%18s' % '-' for c in cols))

@@ -20,7 +20,7 @@ def short(name):
     m = re.search(r'conv_kernelI(?:DF16b|DF16_|f)Li(\d+)E', name)
     if m:
         return LAYERS[int(m.group(1))]
-    if 'down0_kernel' in name:
+    if 'down0_kernel' in name or 'down0_mfma_kernel' in name:
         return 'down0'
     # rocprofv3 demangles conv_kernel<__bf16, 1, XS> as 'conv_kernel<bool _Accum, int, E, XS>' (before the
     # XS parameter existed: 'conv_kernel<bool _Accum, int, E>'); of the 16-bit conv kinds a generate
