@@ -78,9 +78,32 @@ template <typename T> struct Frag;
 template <> struct Frag<bf16> { typedef bf16x8 type; };
 template <> struct Frag<f16> { typedef f16x8 type; };
 template <> struct Frag<float> { typedef bf16x8 type; };   // unused by the f32 path
+#if CONV_EXP_MODE & 256
+// diagnostic (conv_micro mode 256, wrong outputs): each 32x32x16 MFMA issued as two 16x16x32 MFMAs on the
+// same operand registers -- the same MFMA cycles and FLOP; does the power-limited clock rise with the shape
+// (MI355X_MICROARCH.md, clocks (7))?
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  typedef float f32x4_ __attribute__((ext_vector_type(4)));
+#if CONV_EXP_MODE & 512   // both on registers 0..3 (a dependent pair: no extra accumulator moves)
+  f32x4_ c0 = __builtin_shufflevector(c, c, 0, 1, 2, 3);
+  c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c0, 0, 0, 0);
+  c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c0, 0, 0, 0);
+  c[0] = c0[0]; c[1] = c0[1]; c[2] = c0[2]; c[3] = c0[3];
+  return c;
+#else
+  f32x4_ c0 = {c[0], c[1], c[2], c[3]}, c1 = {c[4], c[5], c[6], c[7]};
+  c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c0, 0, 0, 0);
+  c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c1, 0, 0, 0);
+  c[0] = c0[0]; c[1] = c0[1]; c[2] = c0[2]; c[3] = c0[3];
+  c[4] = c1[0]; c[5] = c1[1]; c[6] = c1[2]; c[7] = c1[3];
+  return c;
+#endif
+}
+#else
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+#endif
 __device__ __forceinline__ f32x16 mfma32(f16x8 a, f16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }

@@ -6,6 +6,7 @@
 #   micro    conv_micro step layers in isolation + stamps (prebuilt binaries)
 #   pmc      rocprofv3 PMC passes (bf16, bf16x3) -> $OUT/pmc_traffic.json (bench.py's per-kernel counters)
 #   cores    scripts/micro/coresident.sh (down1 co-residency experiment, prebuilt binaries)
+#   ldspmc   one rocprofv3 PMC pass of the LDS counters per network (bank conflicts per kernel)
 #   bench    the driver's bench command (1 GPU) and a rocprofv3 kernel-stats pass
 #   ab       REPS interleaved bench pairs: this build vs each ALT build and each ALTENVS setting (VAR=value)
 # Usage: ALTS="pre_prune.so" STAGES="bitwise tests" bash scripts/gpu_r4.sh TAG
@@ -46,8 +47,13 @@ fi
 if has micro; then
   # conv_micro (prebuilt: MODES="0 128" bash scripts/micro/build.sh): the 16-bit step layers in isolation, with
   # per-workgroup s_memrealtime stamps in mode 128 (prologue / loop / epilogue; the final level's epilogue parts)
-  (cd scripts/micro && timeout -k 10 120 ./conv_micro_m0 1024 f && timeout -k 10 120 ./conv_micro_m128 1024 f && \
-   timeout -k 10 120 ./conv_micro_m0 1024 x && timeout -k 10 120 ./conv_micro_m128 1024 x) > $OUT/micro.txt 2>&1 || { echo "micro failed"; tail $OUT/micro.txt; exit 1; }
+  # MICRO_MODES: the prebuilt modes to run (default "0 128")
+  : > $OUT/micro.txt
+  for sel in f x; do
+    for m in ${MICRO_MODES:-0 128}; do
+      (cd scripts/micro && timeout -k 10 120 ./conv_micro_m$m 1024 $sel) >> $OUT/micro.txt 2>&1 || { echo "micro failed"; tail $OUT/micro.txt; exit 1; }
+    done
+  done
   grep -E "us|mode" $OUT/micro.txt | head -40
 fi
 if has pmc; then
@@ -58,6 +64,16 @@ if has pmc; then
   BENCH_EXTRA="--dtype bf16x3" bash scripts/gpu_pmc.sh ${TAG}_pmc_x3 || exit 1
   python scripts/pmc_summary.py gpurun_out/${TAG}_pmc_x3 gpurun_out/${TAG}_pmc_x3/pmc.json --traffic --dtype=bf16x3 > gpurun_out/${TAG}_pmc_x3/summary.txt 2>&1 || exit 1
   cp profiles/pmc_traffic.json $OUT/pmc_traffic.json
+fi
+if has ldspmc; then
+  # one PMC pass (LDS counters) per network: a quick bank-conflict check without the full pmc stage
+  for d in bfloat16 bf16x3; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_LDS_UNALIGNED_STALL \
+      -d $GRAFT_REPO_ROOT/$OUT/lds_$d/p1 -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 \
+      --reverse-steps 20 --no-cpu-baseline --no-kernel-timing --dtype $d > $OUT/lds_$d.log 2>&1 || { echo "lds pmc failed"; exit 1; }
+    python scripts/pmc_summary.py $OUT/lds_$d > $OUT/lds_$d.txt 2>&1 || exit 1
+    grep -E "^(down|up)" $OUT/lds_$d.txt
+  done
 fi
 if has bench; then
   timeout -k 10 500 python bench.py --gpus 1 --steps 20 --warmup 5 ${BENCH_EXTRA} > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail $OUT/bench.err; exit 1; }

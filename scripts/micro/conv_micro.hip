@@ -204,6 +204,74 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
                                : 2.0 * rows_out * cout * (double)(c1 + c2) * G::TAPS;
   printf("%-12s mode %d  %8.2f us  %7.1f TF/s (executed)  grid %d\n", name, CONV_EXP_MODE, us, (XS ? 3 : 1) * flop / us * 1e-6,
          ((B + G::S - 1) / G::S) * (cout / G::NT));
+  if (getenv("MICRO_2S")) {
+    // Split-batch experiment: the same B samples as two halves on two streams (a graph of `iters` launch
+    // pairs, fork / join by events), against one stream of whole-batch launches in a graph.  Do the halves'
+    // phases (DMA prologue, MFMA loop, store epilogue) desynchronise and overlap across the chip?
+    const int B1 = B / 2, B2 = B - B1;
+    ConvArgs<bf16> a1 = a, a2 = a;
+    a1.B = B1;
+    a2.B = B2;
+    a2.src1 = s1 + (size_t)B1 * G::LIN * c1 * RS;
+    if (c2) a2.src2 = s2 + (size_t)B1 * (G::FUSED ? G::LH : G::LIN) * c2 * RS;
+    a2.out = out + (size_t)B1 * G::L * cout * RS;
+    a2.out_pool = pool + (size_t)B1 * (G::L / 2) * cout * RS;
+    a2.fin.x_t = xt + (size_t)B1 * 96;
+    a2.fin.x_next = xn + (size_t)B1 * 96;
+    a1.fin.next.B = B1;
+    a2.fin.next.B = B2;
+    a2.fin.next.s0 = s0n + (size_t)B1 * 48 * 128 * RS;
+    a2.fin.next.p0 = p0n + (size_t)B1 * 24 * 128 * RS;
+    hipStream_t sa, sb;
+    CK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+    hipEvent_t fk, jn;
+    CK(hipEventCreateWithFlags(&fk, hipEventDisableTiming));
+    CK(hipEventCreateWithFlags(&jn, hipEventDisableTiming));
+    auto capture = [&](bool split) {
+      hipGraph_t g;
+      hipGraphExec_t ge;
+      CK(hipStreamBeginCapture(sa, hipStreamCaptureModeThreadLocal));
+      if (split) {
+        CK(hipEventRecord(fk, sa));
+        CK(hipStreamWaitEvent(sb, fk, 0));
+      }
+      for (int i = 0; i < iters; ++i) {
+        if (split) {
+          CK(launch_conv<bf16>(KIND, a1, sa, XS != 0));
+          CK(launch_conv<bf16>(KIND, a2, sb, XS != 0));
+        } else {
+          CK(launch_conv<bf16>(KIND, a, sa, XS != 0));
+        }
+      }
+      if (split) {
+        CK(hipEventRecord(jn, sb));
+        CK(hipStreamWaitEvent(sa, jn, 0));
+      }
+      CK(hipStreamEndCapture(sa, &g));
+      CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+      CK(hipGraphDestroy(g));
+      return ge;
+    };
+    double t[2];
+    for (int split = 0; split < 2; ++split) {
+      hipGraphExec_t ge = capture(split != 0);
+      CK(hipGraphLaunch(ge, sa));
+      CK(hipStreamSynchronize(sa));
+      CK(hipEventRecord(e0, sa));
+      CK(hipGraphLaunch(ge, sa));
+      CK(hipEventRecord(e1, sa));
+      CK(hipEventSynchronize(e1));
+      float gms;
+      CK(hipEventElapsedTime(&gms, e0, e1));
+      t[split] = gms * 1e3 / iters;
+      CK(hipGraphExecDestroy(ge));
+    }
+    printf("   graph of %d launches: one stream %.2f us / batch | two streams x B/2 %.2f us / batch (%+.1f %%)\n", iters,
+           t[0], t[1], 100.0 * (t[0] / t[1] - 1.0));
+    CK(hipStreamDestroy(sa));
+    CK(hipStreamDestroy(sb));
+  }
   hipFree(s1); if (s2) hipFree(s2); hipFree(w); hipFree(out); hipFree(pool); hipFree(cmap); hipFree(tmap);
   hipFree(bias); hipFree(wf); hipFree(bfv); hipFree(xt); hipFree(xn); hipFree(tab); hipFree(rng); hipFree(dbg);
   hipFree(ep); hipFree(w0); hipFree(m0c); hipFree(m0t); hipFree(s0n); hipFree(p0n);
