@@ -38,6 +38,10 @@
 // the prologue DMA, bit 32 drops the ring barriers, bit 64 the
 // fragment reads (MFMAs on register operands), bit 128 stamps the main loop's
 // cycles and clock into fin.x_all.  The product is built with 0.
+// 16x16x32 MFMAs on the 16-bit (non-bf16x3) layers that have an M16 K loop (1; 0: 32x32x16 everywhere)
+#ifndef CONV_M16
+#define CONV_M16 1
+#endif
 #ifndef CONV_EXP_MODE
 #define CONV_EXP_MODE 0
 #endif
@@ -108,6 +112,45 @@ __device__ __forceinline__ f32x16 mfma32(f16x8 a, f16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+// 16x16x32 MFMA (M16 layers): under the power-limited clock the chip holds a higher clock on this shape than
+// on 32x32x16 for the same FLOP (MI355X_MICROARCH.md clocks (7); conv_micro mode 768: up0 1.65 -> 1.91 GHz).
+// A 32 x 32 accumulator tile keeps its f32x16, as four 16 x 16 blocks: block BLK = 2 rh + ch (row half rh,
+// column half ch) in registers 4 BLK .. 4 BLK + 3; lane l holds rows 4 (l >> 4) + q, column l & 15 of its block.
+// An operand fragment covers 16 rows (columns) x 32 k: lane l reads row l & 15, 16-B piece l >> 4 of a 64-B row.
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+template <int BLK, typename F>
+__device__ __forceinline__ void mfma16_blk(f32x16& c, F a, F b) {
+  f32x4 t = {c[4 * BLK], c[4 * BLK + 1], c[4 * BLK + 2], c[4 * BLK + 3]};
+  t = mfma16(a, b, t);
+  c[4 * BLK] = t[0];
+  c[4 * BLK + 1] = t[1];
+  c[4 * BLK + 2] = t[2];
+  c[4 * BLK + 3] = t[3];
+}
+// The M16 accumulator of a 32 x 32 tile: its four blocks as separate f32x4 values (an f32x16 sliced by the
+// MFMAs costs the one-wave fused kernels accumulator copies between AGPR tuples); e -> block e >> 2, reg e & 3
+struct Acc16 {
+  f32x4 b[4];
+  __device__ __forceinline__ float operator[](int e) const { return b[e >> 2][e & 3]; }
+};
+template <int BLK, typename F>
+__device__ __forceinline__ void mfma16_blk(Acc16& c, F a, F b) {
+  c.b[BLK] = mfma16(a, b, c.b[BLK]);
+}
+// accumulator register e of a 32 x 32 tile -> its row / column in the tile (32x32x16 or M16 layout)
+template <bool M16>
+__device__ __forceinline__ int acc_row(int e, int lane) {
+  return M16 ? 16 * (e >> 3) + 4 * (lane >> 4) + (e & 3) : 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3);
+}
+template <bool M16>
+__device__ __forceinline__ int acc_col(int e, int lane) {
+  return M16 ? 16 * ((e >> 2) & 1) + (lane & 15) : (lane & 31);
+}
 // TR: the transposed product C^T += B^T A^T (the operands' roles swapped), so the accumulator of a 32 x 32
 // tile holds one tile ROW per lane and 16 output channels in its registers (the final level's
 // register-direct final conv).  Each output element takes the same products in the same k order.
@@ -842,6 +885,10 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   // fused final level: transposed accumulators (mfma_ab), one tile row per lane, so the final 1x1 conv
   // runs from the registers without staging the C tile (the unfused final level keeps the staged rows)
   constexpr bool TF = G::FIN_MAPS;
+  // 16x16x32 K loop (see mfma16): the position-major layers, 16-bit, not bf16x3
+  constexpr bool UC = G::FUSED && G::S == 16 && sizeof(T) == 2 && G::STAGES == 3;   // up1: A cache by key
+  // (down1's generic row path on 16x16x32 measured slower: 14.2 vs 13.3 us, at 256 VGPRs; it stays on 32x32x16)
+  constexpr bool M16 = CONV_M16 && sizeof(T) == 2 && XS == 0 && (G::PM || G::W6 || UC);
   const int NC = P3 ? (a.c1 + a.c2) / (G::KC / 2) : (XS ? 3 : 1) * (a.c1 / G::KC + a.c2 / G::KC);
 
   // Final level: this thread's output row (one per thread) and every global operand of its
@@ -904,11 +951,13 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       aoff[j][i] = (G::FUSED && row == G::ZROW) ? G::ZOFF + (c0 << 4) : row * ROWB + ((c0 ^ G::key(row)) << 4);
     }
   }
+  // M16 rows / columns: lane & 15 of a 16-row half, piece lane >> 4 (the other half: + 16 rows)
+  const int qrl = M16 ? (lane & 15) : lr, qpc = M16 ? (lane >> 4) : c0;
   int boff[2];
 #pragma unroll
   for (int jn = 0; jn < 2; ++jn) {
-    const int n = wn * 64 + jn * 32 + lr;
-    boff[jn] = G::A_BYTES + n * ROWB + ((c0 ^ G::key(n)) << 4);
+    const int n = wn * 64 + jn * 32 + qrl;
+    boff[jn] = G::A_BYTES + n * ROWB + ((qpc ^ G::key(n)) << 4);
   }
   // Fused segment 2: composite tap k of output row (s, l = 2m + e) reads coarse row m - 1 + k;
   // B holds both phases' taps, a wave reads its own phase's.  The m = 0 rows also take the
@@ -929,14 +978,33 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       }
     }
     {
-      const int r = G::frag_row(wm, 0) + lr;
+      const int r = G::frag_row(wm, 0) + qrl;
       const int sq = r % G::S, m = (r / G::S) % G::LH, row = sq;
-      amask = m == 0 ? row * ROWB + ((c0 ^ G::key(row)) << 4) : G::ZOFF + (c0 << 4);
+      amask = m == 0 ? row * ROWB + ((qpc ^ G::key(row)) << 4) : G::ZOFF + (qpc << 4);
     }
 #pragma unroll
     for (int jn = 0; jn < 2; ++jn) {
-      const int n = wn * 64 + jn * 32 + lr;
-      boff2[jn] = G::A2_BYTES + (ph * G::TAPS2 * NT + n) * ROWB + ((c0 ^ G::key(n)) << 4);
+      const int n = wn * 64 + jn * 32 + qrl;
+      boff2[jn] = G::A2_BYTES + (ph * G::TAPS2 * NT + n) * ROWB + ((qpc ^ G::key(n)) << 4);
+    }
+  }
+  // up1 on M16: the A offset of every cache key -- segment 1: fine position 2 mb + e - PADL + key, segment 2:
+  // coarse row mb - 1 + key (mb: fragment 0's first coarse row, e: the wave's output phase); zero row outside
+  constexpr int UK1 = (UC && M16) ? 16 : 1, UK2 = (UC && M16) ? 9 : 1;
+  int akey1[UK1], akey2[UK2];
+  if constexpr (UC && M16) {
+    const int e = (wm * 96) / G::PHROWS, mb = ((wm * 96) % G::PHROWS) / G::S;
+#pragma unroll
+    for (int k = 0; k < UK1; ++k) {
+      const int p = 2 * mb + e - PADL + k;
+      const int row = G::slot1(p, qrl);
+      akey1[k] = (p >= 0 && p < L) ? row * ROWB + ((qpc ^ G::key(row)) << 4) : G::ZOFF + (qpc << 4);
+    }
+#pragma unroll
+    for (int k = 0; k < UK2; ++k) {
+      const int q = mb - 1 + k;
+      const int row = q * G::S + qrl;
+      akey2[k] = (q >= 0 && q < G::LH) ? row * ROWB + ((qpc ^ G::key(row)) << 4) : G::ZOFF + (qpc << 4);
     }
   }
   // up0.fused (W6): wave = (phase w6e, column half w6h); A offsets per input position of the lane's sample
@@ -944,18 +1012,19 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   constexpr int W6P1 = G::W6 ? G::L : 1, W6P2 = G::W6 ? G::LH : 1;
   int apos1[W6P1], apos2[W6P2];
   if constexpr (G::W6) {
-    const int n = w6h * 32 + lr;
-    boff[0] = G::A_BYTES + n * ROWB + ((c0 ^ G::key(n)) << 4);
-    boff2[0] = G::A2_BYTES + (w6e * G::TAPS2 * NT + n) * ROWB + ((c0 ^ G::key(n)) << 4);
+    // (M16: row / column l & 15 of a 16-row half, piece l >> 4; the other half is + 16 rows, as in the PM path)
+    const int n = w6h * 32 + qrl;
+    boff[0] = G::A_BYTES + n * ROWB + ((qpc ^ G::key(n)) << 4);
+    boff2[0] = G::A2_BYTES + (w6e * G::TAPS2 * NT + n) * ROWB + ((qpc ^ G::key(n)) << 4);
 #pragma unroll
     for (int p = 0; p < G::L; ++p) {
-      const int row = G::slot1(p, lr);
-      apos1[p] = row * ROWB + ((c0 ^ G::key(row)) << 4);
+      const int row = G::slot1(p, qrl);
+      apos1[p] = row * ROWB + ((qpc ^ G::key(row)) << 4);
     }
 #pragma unroll
     for (int q = 0; q < G::LH; ++q) {
-      const int row = q * G::S + lr;
-      apos2[q] = row * ROWB + ((c0 ^ G::key(row)) << 4);
+      const int row = q * G::S + qrl;
+      apos2[q] = row * ROWB + ((qpc ^ G::key(row)) << 4);
     }
     amask = apos2[0];
   }
@@ -964,23 +1033,24 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   constexpr int PW6P = G::PM ? G::L : 1;
   int apm[PW6P];
   if constexpr (G::PM) {
-    const int n = w6h * 32 + lr;
-    boff[0] = G::A_BYTES + n * ROWB + ((c0 ^ G::key(n)) << 4);
-    const int sm = (pw6set & (G::L == 6 ? 1 : 0)) * 32 + lr;   // sample of this lane (down3: half pw6set)
+    // M16: lane l reads row / column l & 15 of a 16-row half, 16-B piece l >> 4 (the other half: + 16 rows,
+    // the same key); 32x32x16: row / column lr, piece h of the k-group's 32-B half
+    const int n = w6h * 32 + qrl;
+    boff[0] = G::A_BYTES + n * ROWB + ((qpc ^ G::key(n)) << 4);
+    const int sm = (pw6set & (G::L == 6 ? 1 : 0)) * 32 + qrl;   // sample of this lane (down3: half pw6set)
 #pragma unroll
     for (int p = 0; p < G::L; ++p) {
       const int row = p * G::S + sm;
-      apm[p] = row * ROWB + ((c0 ^ G::key(row)) << 4);
+      apm[p] = row * ROWB + ((qpc ^ G::key(row)) << 4);
     }
   }
 
-  f32x16 acc[3][2];
+  using AccT = std::conditional_t<M16, Acc16, f32x16>;
+  AccT acc[3][2];
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
-    for (int jn = 0; jn < 2; ++jn)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][jn][e] = 0.f;
+    for (int jn = 0; jn < 2; ++jn) acc[i][jn] = AccT{};
 
   DmaPlan<T, KIND, XS> dma;
   dma.init(a, m0, n_tile, NC, wv, lane);
@@ -995,11 +1065,12 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   // (sched_group_barrier: M R M R M R M R M R M V), so no gap carries more than one
   // ds_read_b128 (MI355X_MICROARCH.md LDS: a third read per gap saturates the array).
   typedef typename Frag<T>::type fragT;
-  fragT av[2][3], bv[2][2];
+  constexpr int NBV = M16 ? 4 : 2;                 // B fragments a step (M16: [jn][column half])
+  fragT av[2][3], bv[2][NBV];
 #pragma unroll
   for (int i = 0; i < 3; ++i) av[1][i] = av[0][i] = fragT{};
 #pragma unroll
-  for (int jn = 0; jn < 2; ++jn) bv[1][jn] = bv[0][jn] = fragT{};
+  for (int jn = 0; jn < NBV; ++jn) bv[1][jn] = bv[0][jn] = fragT{};
   if constexpr ((CONV_EXP_MODE & 64) != 0) {   // diagnostic: non-zero register operands
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -1011,13 +1082,17 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   constexpr bool ZAP = G::W6 || G::PM;
   constexpr int ZAP_H = ZAP ? 2 : 1, ZAP_P = ZAP ? G::L : 1;
   fragT zap[ZAP_H][ZAP_P];
-  // up1 A cache: [32-B half][key 4 i + j (segment 1, 14 keys) / 2 i + k (segment 2, 8)]
-  constexpr bool UC = G::FUSED && G::S == 16 && sizeof(T) == 2 && G::STAGES == 3;
-  fragT uca[UC ? 2 : 1][UC ? 14 : 1];
+  // up1 A cache: [32-B half][key 4 i + j (segment 1, 14 keys) / 2 i + k (segment 2, 8)]; M16: ucm[key] of the
+  // 16-row halves, key 4 i + 2 rh + j (segment 1, 16 keys) / 2 i + rh + k (segment 2, 9)
+  constexpr bool UCO = UC && !M16;
+  fragT uca[UCO ? 2 : 1][UCO ? 14 : 1];
 #pragma unroll
-  for (int hh = 0; hh < (UC ? 2 : 1); ++hh)
+  for (int hh = 0; hh < (UCO ? 2 : 1); ++hh)
 #pragma unroll
-    for (int p = 0; p < (UC ? 14 : 1); ++p) uca[hh][p] = fragT{};
+    for (int p = 0; p < (UCO ? 14 : 1); ++p) uca[hh][p] = fragT{};
+  fragT ucm[UC && M16 ? 16 : 1];
+#pragma unroll
+  for (int p = 0; p < (UC && M16 ? 16 : 1); ++p) ucm[p] = fragT{};
 #pragma unroll
   for (int hh = 0; hh < ZAP_H; ++hh)
 #pragma unroll
@@ -1027,7 +1102,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int jn = 0; jn < 2; ++jn)
-        if constexpr (sizeof(T) == 2 && !(CONV_EXP_MODE & 2))
+        if constexpr (sizeof(T) == 2 && !M16 && !(CONV_EXP_MODE & 2))
           acc[i][jn] = mfma_ab<TF>(av[pb][i], bv[pb][jn], acc[i][jn]);
   };
   // Fused: left-edge correction weights of this lane (registers, one chunk ahead), see has_m0
@@ -1039,10 +1114,18 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   if constexpr (G::FUSED) {
     const int n2 = P3 ? a.c2 / (G::KC / 2) : (XS ? 3 : 1) * (a.c2 / G::KC);
     ebase = reinterpret_cast<const char*>(a.epack) +
-            ((size_t)n_tile * n2 * 2 * NT + (size_t)ph * NT + (G::W6 ? (wv & 1) * 32 : wn * 64) + lr) * ROWB + h * 16;
+            ((size_t)n_tile * n2 * 2 * NT + (size_t)ph * NT + (G::W6 ? (wv & 1) * 32 : wn * 64) + (M16 ? (lane & 15) : lr)) * ROWB +
+            (M16 ? (lane >> 4) : h) * 16;
   }
   auto load_epk = [&](int kc2) {   // segment-2 chunk kc2's correction fragments
-    if constexpr (G::FUSED) {
+    if constexpr (G::FUSED && M16) {   // epk[ch][jn]: column half ch of fragment jn, the whole 64-B row
+      const char* p = ebase + (size_t)kc2 * 2 * NT * ROWB;
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+        for (int jn = 0; jn < (G::W6 ? 1 : 2); ++jn)
+          epk[ch][jn] = *reinterpret_cast<const fragT*>(p + jn * 32 * ROWB + ch * 16 * ROWB);
+    } else if constexpr (G::FUSED) {
       const char* p = ebase + (size_t)kc2 * 2 * NT * ROWB;
 #pragma unroll
       for (int g = 0; g < NGE; ++g)
@@ -1058,7 +1141,102 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     constexpr int SEGV = (int)decltype(seg_tag)::value;
     constexpr int SEG = SEGV == 4 ? 2 : SEGV;
     char* nbase = smem + nbuf * G::STAGE;
-    if constexpr (G::W6) {
+    if constexpr (G::W6 && M16) {
+      // up0.fused on 16x16x32: step st = tap zs_tap(jj) (one k = 32 step per tap); reads: the step's two B
+      // column halves, then both row halves of the positions first needed at this tap; MFMAs of step st - 1:
+      // fragment f's four blocks, A from zap[rh][position].  Segment 2's left-edge correction: coarse row 0's
+      // halves read at step 0, multiplied into fragment 0 at step 1 (4 MFMAs, epk[0][ch]).
+      static_assert(ROWB == 64, "M16: one 64-B row per step");
+      constexpr int PAT = decltype(pat_tag)::value;
+      constexpr int NT_ = SEG == 2 ? G::TAPS2 : TAPS;
+      constexpr int NS = NT_;
+      constexpr int NPER = NEXT == 3 ? G::PER2 : G::PER;
+      constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;
+      constexpr int PPS = (NPC + NS - 1) / NS;
+      constexpr int HALF = 16 * ROWB;
+      static_assert(NS % 2 == 0, "B double buffer alternates per step");
+      fragT am[SEG == 2 ? 2 : 1];
+      static_for<0, NS>([&](auto st_tag) {
+        constexpr int st = decltype(st_tag)::value;
+        constexpr int jj = st, sb = st & 1, pb = sb ^ 1;
+        constexpr int j = G::zs_tap(SEG, jj);
+        constexpr int jpp = G::zs_tap(SEG, st == 0 ? NS - 1 : st - 1);
+        const char* pb0 = base + (SEG == 2 ? boff2[0] : boff[0]) + j * NT * ROWB;
+        auto body = [&](auto prev_tag) {
+          constexpr int PV = decltype(prev_tag)::value;   // 0: this segment's step st - 1; 1 / 2: segment 1's / 2's last
+          constexpr int SP = PV == 0 ? SEG : PV;
+          constexpr int TPP = PV == 0 ? jpp : SP == 2 ? G::TAPS2 - 1 : TAPS - 1;
+#define PETDIFF_WMF(f)                                                                                      \
+  if constexpr (G::w6_ok(SP, PAT, f, TPP) && !(CONV_EXP_MODE & 2)) {                                        \
+    constexpr int P_ = G::w6_pos(SP, PAT, f, TPP);                                                           \
+    mfma16_blk<0>(acc[(f) % 3][(f) / 3], zap[0][P_], bv[pb][0]);                                             \
+    mfma16_blk<1>(acc[(f) % 3][(f) / 3], zap[0][P_], bv[pb][1]);                                             \
+    mfma16_blk<2>(acc[(f) % 3][(f) / 3], zap[1][P_], bv[pb][0]);                                             \
+    mfma16_blk<3>(acc[(f) % 3][(f) / 3], zap[1][P_], bv[pb][1]);                                             \
+  }
+#define PETDIFF_WRA(f)                                                                                      \
+  if constexpr (G::w6_ok(SEG, PAT, f, j) && G::w6_first(SEG, PAT, f, jj) && !(CONV_EXP_MODE & 64)) {        \
+    constexpr int P_ = G::w6_pos(SEG, PAT, f, j);                                                            \
+    const int ao_ = SEG == 2 ? apos2[P_ < G::LH ? P_ : 0] : apos1[P_];                                       \
+    zap[0][P_] = *reinterpret_cast<const fragT*>(base + ao_);                                                \
+    zap[1][P_] = *reinterpret_cast<const fragT*>(base + ao_ + HALF);                                         \
+  }
+          // fragment f's reads go after fragment min(f + 2, 5)'s MFMAs, and after the last MFMA of the step
+          // that still multiplies the zap entry they replace (both row halves of a position share a slot)
+          constexpr auto slot = [](int f) {
+            int g = f + 2 < 5 ? f + 2 : 5;
+            for (int f2 = 0; f2 < 6; ++f2)
+              if (G::w6_ok(SP, PAT, f2, TPP) && G::w6_pos(SP, PAT, f2, TPP) == G::w6_pos(SEG, PAT, f, j) && f2 > g) g = f2;
+            return g;
+          };
+          static_for<0, 6>([&](auto g_tag) {
+            constexpr int g = decltype(g_tag)::value;
+            PETDIFF_WMF(g)
+            if constexpr (g == 0 && !(CONV_EXP_MODE & 64)) bv[sb][0] = *reinterpret_cast<const fragT*>(pb0);
+            if constexpr (g == 1 && !(CONV_EXP_MODE & 64)) bv[sb][1] = *reinterpret_cast<const fragT*>(pb0 + HALF);
+            static_for<0, 6>([&](auto f_tag) {
+              constexpr int f = decltype(f_tag)::value;
+              if constexpr (slot(f) == g) { PETDIFF_WRA(f) }
+            });
+            __builtin_amdgcn_sched_barrier(0);
+          });
+#undef PETDIFF_WRA
+#undef PETDIFF_WMF
+        };
+        if constexpr (st > 0) body(std::integral_constant<int, 0>{});
+        else if constexpr (SEG == 1 || SEGV == 4) body(std::integral_constant<int, 1>{});
+        else body(std::integral_constant<int, 2>{});
+        if constexpr (SEG == 2) {
+          if (st == 0) {
+            am[0] = *reinterpret_cast<const fragT*>(base + amask);
+            am[1] = *reinterpret_cast<const fragT*>(base + amask + HALF);
+          }
+          if (st == 1) {
+            if constexpr (!(CONV_EXP_MODE & 2)) {
+              mfma16_blk<0>(acc[0][0], am[0], epk[0][0]);
+              mfma16_blk<1>(acc[0][0], am[0], epk[1][0]);
+              mfma16_blk<2>(acc[0][0], am[1], epk[0][0]);
+              mfma16_blk<3>(acc[0][0], am[1], epk[1][0]);
+            }
+            const int k2 = kc - dma.n1;
+            if (kc + 1 < NC) load_epk(k2 + 1);
+          }
+        }
+        if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
+#pragma unroll
+          for (int u = 0; u < PPS; ++u) {
+            const int k = st * PPS + u;
+            if (k < NPER) {
+              if constexpr (NEXT == 3) dma.piece2(nbase, k, nkc - dma.n1, lane);
+              else dma.piece1(nbase, k, nkc, lane);
+            } else if (NEXT == 2 && k < NPC) {
+              dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    } else if constexpr (G::W6) {
       // up0.fused, 6 fragments per wave: wave (phase PAT, column half); step st = (k-group
       // g, tap zs_tap(jj)); reads: the step's B fragment, then the positions first needed at this tap in the
       // first group of their A half; MFMAs of step st - 1: fragment f -> acc[f % 3][f / 3], A from zap.
@@ -1146,6 +1324,68 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         }
         __builtin_amdgcn_sched_barrier(0);
       });
+    } else if constexpr (G::PM && M16) {
+      // position-major on 16x16x32: step st = tap j (the whole 64-B row is one k = 32 step); reads: the
+      // step's two B column halves, then both row halves of the set's positions first needed at tap j;
+      // MFMAs of step st - 1: fragment f's four blocks (rh, ch), A from zap[rh][position].
+      static_assert(ROWB == 64, "M16: one 64-B row per step");
+      constexpr int NS = TAPS;
+      constexpr int NPER = G::PER;
+      constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;
+      constexpr int PPS = (NPC + NS - 1) / NS;
+      constexpr int SET = decltype(pat_tag)::value;
+      constexpr int HALF = 16 * ROWB;                     // + 16 rows: the other row / column half
+      static_assert(NS % 2 == 0, "B double buffer alternates per step");
+      static_for<0, NS>([&](auto st_tag) {
+        constexpr int st = decltype(st_tag)::value;
+        constexpr int j = st, sb = st & 1, pb = sb ^ 1;
+        constexpr int jp = st == 0 ? TAPS - 1 : st - 1;
+        const char* pb0 = base + boff[0] + j * NT * ROWB;
+#define PETDIFF_QMF(f, rh, ch)                                                                              \
+  if constexpr (G::pw6_valid(SET, f, jp) && !(CONV_EXP_MODE & 2))                                           \
+    mfma16_blk<2 * (rh) + (ch)>(acc[(f) % 3][(f) / 3], zap[rh][G::pw6_pos(SET, f) + jp - PADL], bv[pb][ch]);
+#define PETDIFF_QRA(f, rh)                                                                                  \
+  if constexpr (G::pw6_valid(SET, f, j) && G::pw6_first(SET, f, j) && !(CONV_EXP_MODE & 64)) {              \
+    constexpr int P_ = G::pw6_pos(SET, f) + j - PADL;                                                        \
+    zap[rh][P_] = *reinterpret_cast<const fragT*>(base + apm[P_] + (rh) * HALF);                             \
+  }
+#define PETDIFF_QF(f)                                                                                       \
+  PETDIFF_QMF(f, 0, 0)                                                                                      \
+  PETDIFF_QMF(f, 0, 1)                                                                                      \
+  PETDIFF_QMF(f, 1, 0)                                                                                      \
+  PETDIFF_QMF(f, 1, 1)
+        // fragment f's reads go after fragment min(f + 2, 5)'s MFMAs, and after the last MFMA of the step
+        // that still multiplies the zap entry they replace (program order decides which value it gets)
+        constexpr auto slot = [](int f) {
+          int g = f + 2 < 5 ? f + 2 : 5;
+          for (int f2 = 0; f2 < 6; ++f2)
+            if (G::pw6_valid(SET, f2, jp) && G::pw6_pos(SET, f2) + jp == G::pw6_pos(SET, f) + j && f2 > g) g = f2;
+          return g;
+        };
+        static_for<0, 6>([&](auto g_tag) {
+          constexpr int g = decltype(g_tag)::value;
+          PETDIFF_QF(g)
+          if constexpr (g == 0 && !(CONV_EXP_MODE & 64)) bv[sb][0] = *reinterpret_cast<const fragT*>(pb0);
+          if constexpr (g == 1 && !(CONV_EXP_MODE & 64)) bv[sb][1] = *reinterpret_cast<const fragT*>(pb0 + HALF);
+          static_for<0, 6>([&](auto f_tag) {
+            constexpr int f = decltype(f_tag)::value;
+            if constexpr (slot(f) == g) { PETDIFF_QRA(f, 0) PETDIFF_QRA(f, 1) }
+          });
+          __builtin_amdgcn_sched_barrier(0);
+        });
+#undef PETDIFF_QF
+#undef PETDIFF_QRA
+#undef PETDIFF_QMF
+        if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
+#pragma unroll
+          for (int u = 0; u < PPS; ++u) {
+            const int k = st * PPS + u;
+            if (k < NPER) dma.piece1(nbase, k, nkc, lane);
+            else if (NEXT == 2 && k < NPC) dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
     } else if constexpr (G::PM) {
       // position-major, 6 fragments per wave: step st = (tap j, k-group g) as the generic
       // paths; reads: the step's B fragment, then the set's positions first needed at tap j (first group of
@@ -1199,6 +1439,102 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
             const int k = st * PPS + u;
             if (k < NPER) dma.piece1(nbase, k, nkc, lane);
             else if (NEXT == 2 && k < NPC) dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    } else if constexpr (UC && M16) {
+      // up1 on 16x16x32: step st = tap j; reads: the step's four B fragments (jn, column half), then the keys
+      // first needed at tap j; MFMAs of step st - 1: fragment (i, rh) x (jn, ch) with A = ucm[key].  Segment
+      // 2's left-edge correction: coarse row 0 (row half 0 of fragment 0) x epk, in has_m0 waves.
+      static_assert(ROWB == 64, "M16: one 64-B row per step");
+      constexpr int NT_ = SEG == 2 ? G::TAPS2 : TAPS;
+      constexpr int NS = NT_;
+      constexpr int NPER = NEXT == 3 ? G::PER2 : G::PER;
+      constexpr int NPC = (NEXT == 2 ? 2 : 1) * NPER;
+      constexpr int PPS = (NPC + NS - 1) / NS;
+      constexpr int KS = SEG == 2 ? 2 : 4, HK = KS / 2;   // key step between fragments / row halves
+      constexpr int HALF = 16 * ROWB;
+      static_assert(NS % 2 == 0, "B double buffer alternates per step");
+      fragT am;
+      static_for<0, NS>([&](auto st_tag) {
+        constexpr int st = decltype(st_tag)::value;
+        constexpr int j = st, sb = st & 1, pb = sb ^ 1;
+        constexpr bool PS1 = st > 0 ? SEG == 1 : (SEG == 1 || SEGV == 4);   // the previous step's segment is 1
+        constexpr int KSP = PS1 ? 4 : 2, HKP = KSP / 2;
+        constexpr int JP = st > 0 ? st - 1 : PS1 ? TAPS - 1 : G::TAPS2 - 1;
+        const char* pb0 = base + (SEG == 2 ? boff2[0] : boff[0]) + j * NT * ROWB;
+        const char* pb1 = base + (SEG == 2 ? boff2[1] : boff[1]) + j * NT * ROWB;
+        // (i, rh) first reads key KS i + HK rh + j unless an earlier tap of this chunk read it
+        auto first = [](int i, int rh) {
+          for (int j2 = 0; j2 < j; ++j2)
+            for (int i2 = 0; i2 < 3; ++i2)
+              for (int r2 = 0; r2 < 2; ++r2)
+                if (KS * i2 + HK * r2 + j2 == KS * i + HK * rh + j) return false;
+          return true;
+        };
+#define PETDIFF_UMF(i, rh)                                                                                  \
+  if constexpr (!(CONV_EXP_MODE & 2)) {                                                                     \
+    constexpr int K_ = KSP * (i) + HKP * (rh) + JP;                                                          \
+    mfma16_blk<2 * (rh)>(acc[i][0], ucm[K_], bv[pb][0]);                                                     \
+    mfma16_blk<2 * (rh) + 1>(acc[i][0], ucm[K_], bv[pb][1]);                                                 \
+    mfma16_blk<2 * (rh)>(acc[i][1], ucm[K_], bv[pb][2]);                                                     \
+    mfma16_blk<2 * (rh) + 1>(acc[i][1], ucm[K_], bv[pb][3]);                                                 \
+  }
+#define PETDIFF_URA(i, rh)                                                                                  \
+  if constexpr (first(i, rh) && !(CONV_EXP_MODE & 64)) {                                                    \
+    constexpr int K_ = KS * (i) + HK * (rh) + j;                                                             \
+    ucm[K_] = *reinterpret_cast<const fragT*>(base + (SEG == 2 ? akey2[K_] : akey1[K_]));                    \
+  }
+#define PETDIFF_URB(q, ptr) \
+  if constexpr (!(CONV_EXP_MODE & 64)) bv[sb][q] = *reinterpret_cast<const fragT*>(ptr);
+        PETDIFF_UMF(0, 0)
+        PETDIFF_URB(0, pb0)
+        __builtin_amdgcn_sched_barrier(0);
+        PETDIFF_UMF(0, 1)
+        PETDIFF_URB(1, pb0 + HALF)
+        __builtin_amdgcn_sched_barrier(0);
+        PETDIFF_UMF(1, 0)
+        PETDIFF_URB(2, pb1)
+        __builtin_amdgcn_sched_barrier(0);
+        PETDIFF_UMF(1, 1)
+        PETDIFF_URB(3, pb1 + HALF)
+        __builtin_amdgcn_sched_barrier(0);
+        PETDIFF_UMF(2, 0)
+        PETDIFF_URA(0, 0)
+        PETDIFF_URA(0, 1)
+        __builtin_amdgcn_sched_barrier(0);
+        PETDIFF_UMF(2, 1)
+        PETDIFF_URA(1, 0)
+        PETDIFF_URA(1, 1)
+        PETDIFF_URA(2, 0)
+        PETDIFF_URA(2, 1)
+#undef PETDIFF_URB
+#undef PETDIFF_URA
+#undef PETDIFF_UMF
+        if constexpr (SEG == 2) {
+          if (st == 0 && has_m0) am = *reinterpret_cast<const fragT*>(base + amask);
+          if (st == 1 && has_m0) {
+            if constexpr (!(CONV_EXP_MODE & 2)) {
+              mfma16_blk<0>(acc[0][0], am, epk[0][0]);
+              mfma16_blk<1>(acc[0][0], am, epk[1][0]);
+              mfma16_blk<0>(acc[0][1], am, epk[0][1]);
+              mfma16_blk<1>(acc[0][1], am, epk[1][1]);
+            }
+            const int k2 = kc - dma.n1;
+            if (kc + 1 < NC) load_epk(k2 + 1);
+          }
+        }
+        if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
+#pragma unroll
+          for (int u = 0; u < PPS; ++u) {
+            const int k = st * PPS + u;
+            if (k < NPER) {
+              if constexpr (NEXT == 3) dma.piece2(nbase, k, nkc - dma.n1, lane);
+              else dma.piece1(nbase, k, nkc, lane);
+            } else if (NEXT == 2 && k < NPC) {
+              dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
+            }
           }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -1597,7 +1933,19 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         buf = buf == 2 ? 0 : buf + 1;
         compute(smem + buf * G::STAGE, No{}, 0, 0, Seg2{}, kc + 1, pat_tag);
         ring_barrier<0>();
-        if constexpr (G::W6) {   // the last chunk's last step (composite tap 3) over this set's valid fragments
+        if constexpr (G::W6 && M16) {   // the last chunk's last step (composite tap 3), four blocks a fragment
+          constexpr int PAT = decltype(pat_tag)::value;
+          static_for<0, 6>([&](auto f_tag) {
+            constexpr int f = decltype(f_tag)::value;
+            if constexpr (G::w6_ok(2, PAT, f, G::TAPS2 - 1) && !(CONV_EXP_MODE & 2)) {
+              constexpr int P_ = G::w6_pos(2, PAT, f, G::TAPS2 - 1);
+              mfma16_blk<0>(acc[f % 3][f / 3], zap[0][P_], bv[1][0]);
+              mfma16_blk<1>(acc[f % 3][f / 3], zap[0][P_], bv[1][1]);
+              mfma16_blk<2>(acc[f % 3][f / 3], zap[1][P_], bv[1][0]);
+              mfma16_blk<3>(acc[f % 3][f / 3], zap[1][P_], bv[1][1]);
+            }
+          });
+        } else if constexpr (G::W6) {   // the last chunk's last step (composite tap 3) over this set's valid fragments
           constexpr int PAT = decltype(pat_tag)::value;
           constexpr int HL = kg_a<P3>((P3 ? 3 : ROWB / 32) - 1) >> 5;
           if constexpr (!(CONV_EXP_MODE & 2)) {
@@ -1662,7 +2010,19 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
           ring_barrier<0>();                               // B(kc+1): own LDS reads done
           buf = buf == 2 ? 0 : buf + 1;
         }
-        if constexpr (G::PM) {   // the last step (tap TAPS - 1) of this set's valid fragments
+        if constexpr (G::PM && M16) {   // the last step (tap TAPS - 1) of this set's valid fragments
+          constexpr int SET = decltype(pat_tag)::value;
+          static_for<0, 6>([&](auto f_tag) {
+            constexpr int f = decltype(f_tag)::value;
+            if constexpr (G::pw6_valid(SET, f, TAPS - 1) && !(CONV_EXP_MODE & 2)) {
+              constexpr int P_ = G::pw6_pos(SET, f) + TAPS - 1 - PADL;
+              mfma16_blk<0>(acc[f % 3][f / 3], zap[0][P_], bv[1][0]);
+              mfma16_blk<1>(acc[f % 3][f / 3], zap[0][P_], bv[1][1]);
+              mfma16_blk<2>(acc[f % 3][f / 3], zap[1][P_], bv[1][0]);
+              mfma16_blk<3>(acc[f % 3][f / 3], zap[1][P_], bv[1][1]);
+            }
+          });
+        } else if constexpr (G::PM) {   // the last step (tap TAPS - 1) of this set's valid fragments
           constexpr int SET = decltype(pat_tag)::value;
           constexpr int HL = kg_a<P3>((P3 ? 3 : ROWB / 32) - 1) >> 5;
 #pragma unroll
@@ -1735,6 +2095,20 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   if (loader) return;   // s_barrier waits only for the waves still running
   if constexpr (G::PM || G::W6) {
     // flushed at the end of the position-major / zero-skip main loop
+  } else if constexpr (UC && M16) {   // the last chunk's last step: composite tap 3, keys 2 i + rh + 3
+    static_for<0, 3>([&](auto i_tag) {
+      constexpr int i = decltype(i_tag)::value;
+      if constexpr (!(CONV_EXP_MODE & 2)) {
+        mfma16_blk<0>(acc[i][0], ucm[2 * i + G::TAPS2 - 1], bv[1][0]);
+        mfma16_blk<1>(acc[i][0], ucm[2 * i + G::TAPS2 - 1], bv[1][1]);
+        mfma16_blk<0>(acc[i][1], ucm[2 * i + G::TAPS2 - 1], bv[1][2]);
+        mfma16_blk<1>(acc[i][1], ucm[2 * i + G::TAPS2 - 1], bv[1][3]);
+        mfma16_blk<2>(acc[i][0], ucm[2 * i + G::TAPS2], bv[1][0]);
+        mfma16_blk<3>(acc[i][0], ucm[2 * i + G::TAPS2], bv[1][1]);
+        mfma16_blk<2>(acc[i][1], ucm[2 * i + G::TAPS2], bv[1][2]);
+        mfma16_blk<3>(acc[i][1], ucm[2 * i + G::TAPS2], bv[1][3]);
+      }
+    });
   } else if constexpr (UC) {   // the last chunk's last step: composite tap 3 of the last group's half
     constexpr int HL = kg_a<P3>((P3 ? 3 : ROWB / 32) - 1) >> 5;
 #pragma unroll
@@ -1799,8 +2173,9 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
           // PW6: fragment f = 3 jn + i is position pw6_pos(pw6set, f) of sample half pw6_sh, at its PM tile row
           const int r = (G::W6    ? w6e * G::PHROWS + (3 * jn + i) * G::S
                          : G::PM ? G::pm_row(G::pw6_pos(pw6set, 3 * jn + i), G::pw6_sh(pw6set) * 32)
-                                  : G::frag_row(wm, i)) + (rg & 3) + 8 * (rg >> 2) + 4 * h - part * PROWS;
-          *reinterpret_cast<float2*>(ct + (r >> 1) * G::CT_LD + (G::W6 || G::PM ? w6h * 32 + lr : wn * 64 + jn * 32 + lr) * 2) =
+                                  : G::frag_row(wm, i)) + acc_row<M16>(rg, lane) - part * PROWS;
+          const int cl = acc_col<M16>(rg, lane);
+          *reinterpret_cast<float2*>(ct + (r >> 1) * G::CT_LD + (G::W6 || G::PM ? w6h * 32 + cl : wn * 64 + jn * 32 + cl) * 2) =
               make_float2(acc[i][jn][rg], acc[i][jn][rg + 1]);
         }
 #if CONV_DOWN1_CORES
