@@ -155,7 +155,14 @@ constexpr int layer_ntile(int kind) { return 64 * layer_tile(kind).wn; }
 // (a_hi, w_hi), (a_hi, w_lo), (a_lo, w_hi) on it, so each byte is staged once (2 x the bf16 chunks).  The
 // 32-B-row final level walks three passes over the channels, (a_hi, w_hi) then (a_hi, w_lo) then
 // (a_lo, w_hi), staging a_hi and w_hi twice (3 x the bf16 chunks).
-constexpr bool x3_paired(int kind) { return layer_tile(kind).rowb == 64; }
+// bf16x3 on the 16x16x32 layers (down2, down3, up0.fused, up1.fused; unet_kernels.hip M16): their chunks walk
+// the three passes (a_hi w_hi, a_hi w_lo, a_lo w_hi) of plain 64-B rows, one k = 32 MFMA step per pass and tap,
+// instead of paired [hi | lo] rows (0: paired chunks on 32x32x16 for every 64-B-row layer)
+#ifndef CONV_M16_X3
+#define CONV_M16_X3 1
+#endif
+constexpr bool m16_kind(int kind) { return kind == LK_DOWN2 || kind == LK_DOWN3 || kind == LK_UP0_F || kind == LK_UP1_F; }
+constexpr bool x3_paired(int kind) { return layer_tile(kind).rowb == 64 && !(CONV_M16_X3 && m16_kind(kind)); }
 template <typename T>
 constexpr int layer_kc(int kind) { return layer_tile(kind).rowb / (int)sizeof(T); }
 

@@ -888,7 +888,9 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   // 16x16x32 K loop (see mfma16): the position-major layers, 16-bit, not bf16x3
   constexpr bool UC = G::FUSED && G::S == 16 && sizeof(T) == 2 && G::STAGES == 3;   // up1: A cache by key
   // (down1's generic row path on 16x16x32 measured slower: 14.2 vs 13.3 us, at 256 VGPRs; it stays on 32x32x16)
-  constexpr bool M16 = CONV_M16 && sizeof(T) == 2 && XS == 0 && (G::PM || G::W6 || UC);
+  constexpr bool M16 = CONV_M16 && sizeof(T) == 2 && (XS == 0 || (CONV_M16_X3 && !P3)) && (G::PM || G::W6 || UC);
+  static_assert(!(G::PM || G::W6 || UC) || sizeof(T) != 2 || M16 == (CONV_M16 && (XS == 0 || CONV_M16_X3)),
+                "the host packs bf16x3 weights of these layers by m16_kind (petdiff_internal.h)");
   const int NC = P3 ? (a.c1 + a.c2) / (G::KC / 2) : (XS ? 3 : 1) * (a.c1 / G::KC + a.c2 / G::KC);
 
   // Final level: this thread's output row (one per thread) and every global operand of its
