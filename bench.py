@@ -259,7 +259,7 @@ def load_pmc(fused_up=False, dtype='bfloat16'):
 
 def pmc_fields(pmc, avg_s):
     """HBM GB/s and MFMA utilisation of the dominant kernel against chip peak.
-    SQ_VALU_MFMA_BUSY_CYCLES = 32 cycles per 32x32x16 MFMA (MI355X_MICROARCH.md), summed over the
+    SQ_VALU_MFMA_BUSY_CYCLES = 32 cycles per 32x32x16 MFMA, 16 per 16x16x32 (the same per FLOP; MI355X_MICROARCH.md), summed over the
     1024 SIMDs.  mfma_util = busy / (1024 x 2.4 GHz x launch time): the MFMA pipes' share of the
     peak-clock cycles (the same ratio as executed FLOP/s / dense peak).  mfma_busy_vs_active divides
     by the kernel's own active cycles instead (GRBM_GUI_ACTIVE / 8 XCDs), which the guide notes
