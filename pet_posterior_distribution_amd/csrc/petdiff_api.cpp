@@ -173,8 +173,6 @@ struct petdiff_ctx {
 
 namespace {
 
-// XOR key of the 16-B piece index within a packed weight row n (= ConvGeom::key)
-int piece_key(int n, int cpr) { return cpr == 4 ? ((n >> 2) & 3) : cpr == 2 ? ((n >> 3) & 1) : ((n >> 1) & 7); }
 
 // K chunks of a packed weight tile in kernel order: (channel chunk, part) with part 0 = the value
 // (bf16x3: its hi half) and 1 = its lo half.  bf16x3 walks every input segment of nc chunks three
@@ -232,11 +230,12 @@ int pack_conv(petdiff_ctx* h, const std::vector<float>& wk_host, int li) {
   if (cl.cin_x % KC != 0) return fail(PETDIFF_ERR_UNSUPPORTED, "channel count not a multiple of the K chunk");
   if (cl.cout % NT != 0) return fail(PETDIFF_ERR_UNSUPPORTED, "cout not a multiple of the N tile");
   const int NC = cl.cin_x / KC, nNT = cl.cout / NT;
+  const bool m16 = CONV_M16 && sizeof(T) == 2 && m16_kind(cl.kind);   // = ConvGeom::M16G (piece_key)
   // the up blocks read [skip | u] from two inputs of cin_x / 2 channels each (run_network's lio)
   const bool two = cl.xoff == 0 && cl.cond_level < 0;
   const auto order = chunk_order(two ? NC / 2 : NC, two ? NC / 2 : 0, h->x3, x3_paired(cl.kind));
   // [n_tile][chunk][tap][n (NT)][CPR x 16-B pieces], piece index XOR-swizzled by n
-  // exactly like ConvGeom::key so a linear LDS-DMA copy yields the swizzled image.
+  // exactly like ConvGeom::key (piece_key) so a linear LDS-DMA copy yields the swizzled image.
   std::vector<H> out((size_t)nNT * order.size() * cl.taps * NT * KC);
   size_t q = 0;
   for (int nt = 0; nt < nNT; ++nt)
@@ -244,7 +243,7 @@ int pack_conv(petdiff_ctx* h, const std::vector<float>& wk_host, int li) {
       for (int j = 0; j < cl.taps; ++j)
         for (int n = 0; n < NT; ++n)
           for (int p = 0; p < CPR; ++p) {
-            const int c = p ^ piece_key(n, CPR);
+            const int c = p ^ piece_key(n, CPR, m16);
             for (int e = 0; e < EPC; ++e) {
               int ch, part;
               chunk_elem(ck, KC, CPR, EPC, c, e, ch, part);
@@ -291,6 +290,7 @@ int pack_fused(petdiff_ctx* h, const std::vector<float>& host, int u) {
   const int ROWB = layer_tile(fl.kind).rowb, KC = layer_kc<T>(fl.kind), NT = layer_ntile(fl.kind);
   const int CPR = ROWB / 16, EPC = 16 / (int)sizeof(T);
   const int n1 = fl.cs / KC, n2 = fl.cb / KC, nNT = fl.cout / NT;
+  const bool m16 = CONV_M16 && sizeof(T) == 2 && m16_kind(fl.kind);   // = ConvGeom::M16G (piece_key)
   if (fl.cs % KC || fl.cb % KC || fl.cout % NT || n1 < 3 || n2 < 2)
     return fail(PETDIFF_ERR_UNSUPPORTED, "fused up level geometry");
   // composite taps on the device (fp64 sums), then packed on the host
@@ -317,7 +317,7 @@ int pack_fused(petdiff_ctx* h, const std::vector<float>& host, int u) {
       for (int j = 0; j < 6; ++j)
         for (int n = 0; n < NT; ++n)
           for (int p = 0; p < CPR; ++p) {
-            const int c = p ^ piece_key(n, CPR);
+            const int c = p ^ piece_key(n, CPR, m16);
             for (int e = 0; e < EPC; ++e) {
               int ci, part;
               chunk_elem(ck, KC, CPR, EPC, c, e, ci, part);
@@ -331,7 +331,7 @@ int pack_fused(petdiff_ctx* h, const std::vector<float>& host, int u) {
       for (int t = 0; t < 8; ++t)
         for (int n = 0; n < NT; ++n)
           for (int p = 0; p < CPR; ++p) {
-            const int c = p ^ piece_key(n, CPR);
+            const int c = p ^ piece_key(n, CPR, m16);
             for (int e = 0; e < EPC; ++e) {
               int cb, part;
               chunk_elem(ck, KC, CPR, EPC, c, e, cb, part);

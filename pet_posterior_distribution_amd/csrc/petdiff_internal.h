@@ -155,6 +155,12 @@ constexpr int layer_ntile(int kind) { return 64 * layer_tile(kind).wn; }
 // (a_hi, w_hi), (a_hi, w_lo), (a_lo, w_hi) on it, so each byte is staged once (2 x the bf16 chunks).  The
 // 32-B-row final level walks three passes over the channels, (a_hi, w_hi) then (a_hi, w_lo) then
 // (a_lo, w_hi), staging a_hi and w_hi twice (3 x the bf16 chunks).
+// 16x16x32 MFMA K loops on the 16-bit down2, down3, up0.fused and up1.fused layers (unet_kernels.hip M16;
+// 0: 32x32x16 everywhere).  Shared with the host: those layers' LDS rows and packed weight rows use the
+// 16-row XOR key (piece_key).
+#ifndef CONV_M16
+#define CONV_M16 1
+#endif
 // bf16x3 on the 16x16x32 layers (down2, down3, up0.fused, up1.fused; unet_kernels.hip M16): their chunks walk
 // the three passes (a_hi w_hi, a_hi w_lo, a_lo w_hi) of plain 64-B rows, one k = 32 MFMA step per pass and tap,
 // instead of paired [hi | lo] rows (0: paired chunks on 32x32x16 for every 64-B-row layer)
@@ -163,6 +169,14 @@ constexpr int layer_ntile(int kind) { return 64 * layer_tile(kind).wn; }
 #endif
 constexpr bool m16_kind(int kind) { return kind == LK_DOWN2 || kind == LK_DOWN3 || kind == LK_UP0_F || kind == LK_UP1_F; }
 constexpr bool x3_paired(int kind) { return layer_tile(kind).rowb == 64 && !(CONV_M16_X3 && m16_kind(kind)); }
+// XOR key of 16-B piece index p within a row (an A row in LDS, a packed weight row n): conflict-free ds_read_b128
+// for the lane groups of MI355X_MICROARCH.md's LDS table.  32x32x16 reads 16 rows of one piece per lane group:
+// (row >> 2) & 3.  The 16x16x32 layers (m16: CONV_M16, 16-bit, m16_kind) read 16 rows x 4 pieces per
+// instruction (lane l: row l & 15, piece l >> 4), whose lane groups {0-3, 12-15, 20-27} ... mix two pieces:
+// 2 ((row >> 2) & 1) (the 32x32 key is 2-way there).
+constexpr int piece_key(int row, int cpr, bool m16) {
+  return (m16 && cpr == 4) ? 2 * ((row >> 2) & 1) : cpr == 4 ? ((row >> 2) & 3) : cpr == 2 ? ((row >> 3) & 1) : ((row >> 1) & 7);
+}
 template <typename T>
 constexpr int layer_kc(int kind) { return layer_tile(kind).rowb / (int)sizeof(T); }
 

@@ -38,10 +38,6 @@
 // the prologue DMA, bit 32 drops the ring barriers, bit 64 the
 // fragment reads (MFMAs on register operands), bit 128 stamps the main loop's
 // cycles and clock into fin.x_all.  The product is built with 0.
-// 16x16x32 MFMAs on the 16-bit (non-bf16x3) layers that have an M16 K loop (1; 0: 32x32x16 everywhere)
-#ifndef CONV_M16
-#define CONV_M16 1
-#endif
 #ifndef CONV_EXP_MODE
 #define CONV_EXP_MODE 0
 #endif
@@ -478,10 +474,13 @@ struct ConvGeom {
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   static_assert(EPI != EPI_FINAL || NT == 128, "final conv needs every channel in the tile");
   // XOR key of the 16-B piece index within a row: conflict-free ds_read_b128 for
-  // 16 consecutive rows (lane groups of MI355X_MICROARCH.md LDS table)
-  static __device__ __forceinline__ int key(int row) {
-    return CPR == 4 ? ((row >> 2) & 3) : CPR == 2 ? ((row >> 3) & 1) : ((row >> 1) & 7);
-  }
+  // 16 consecutive rows (lane groups of MI355X_MICROARCH.md LDS table).  The 16x16x32 layers (M16G, see
+  // conv_body's M16) read 16 rows x 4 pieces per instruction, lane l = row l & 15, piece l >> 4: the b128 lane
+  // groups {0-3, 12-15, 20-27} ... then mix two pieces, and (row >> 2) & 3 puts rows 0-3 / 4-7 of pieces 0 / 1
+  // on the same banks (2-way); 2 ((row >> 2) & 1) is conflict-free for that pattern
+  static constexpr bool M16G = CONV_M16 && sizeof(T) == 2 && (PM || W6 || (FUSED && S == 16 && STAGES == 3));
+  static_assert(M16G == (CONV_M16 && sizeof(T) == 2 && m16_kind(KIND)), "host and kernel agree on the 16x16x32 layers");
+  static __device__ __forceinline__ int key(int row) { return piece_key(row, CPR, M16G); }
   // fused segment 1: LDS slot of input position p of sample s -- even positions first, then
   // odd ones, sample-minor: the lanes of a fragment (one output phase, consecutive m or s)
   // then read consecutive slots (conflict-free ds_read_b128 with key())
