@@ -29,6 +29,11 @@
 // The fused final level's time / label map rows: 0 = read from L2 by the transposed final conv in the
 // epilogue, 1 = staged in LDS by LDS-DMA at kernel start (54 KB in the start-up burst of all 256
 // workgroups; A/B: 5035-5051 vs 5093 samples/s for 0, profiles/r04/ab_r4d)
+// 16x16x32 fused levels (up0, up1): the step's LDS-DMA pieces issued between its fragment groups' MFMAs
+// (1) or after all of them (0)
+#ifndef CONV_DMA_SPREAD
+#define CONV_DMA_SPREAD 1
+#endif
 #ifndef CONV_FIN_LDS_MAPS
 #define CONV_FIN_LDS_MAPS 0
 #endif
@@ -1157,6 +1162,25 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       constexpr int HALF = 16 * ROWB;
       static_assert(NS % 2 == 0, "B double buffer alternates per step");
       fragT am[SEG == 2 ? 2 : 1];
+      // the step's DMA pieces: piece u after fragment group dma_g(u) (CONV_DMA_SPREAD), else after the step
+      auto dma_piece = [&](int st, int u) {
+        if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
+          const int k = st * PPS + u;
+          if (k < NPER) {
+            if constexpr (NEXT == 3) dma.piece2(nbase, k, nkc - dma.n1, lane);
+            else dma.piece1(nbase, k, nkc, lane);
+          } else if (NEXT == 2 && k < NPC) {
+            dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
+          }
+        }
+      };
+      auto dma_step = [&](auto st_tag, auto g_tag) {
+        constexpr int st = decltype(st_tag)::value, g = decltype(g_tag)::value;
+        static_for<0, PPS>([&](auto u_tag) {
+          constexpr int u = decltype(u_tag)::value;
+          if constexpr ((u * 6) / PPS + 1 == g || (g == 5 && (u * 6) / PPS + 1 > 5)) dma_piece(st, u);
+        });
+      };
       static_for<0, NS>([&](auto st_tag) {
         constexpr int st = decltype(st_tag)::value;
         constexpr int jj = st, sb = st & 1, pb = sb ^ 1;
@@ -1199,6 +1223,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
               constexpr int f = decltype(f_tag)::value;
               if constexpr (slot(f) == g) { PETDIFF_WRA(f) }
             });
+            if constexpr (CONV_DMA_SPREAD) dma_step(st_tag, g_tag);
             __builtin_amdgcn_sched_barrier(0);
           });
 #undef PETDIFF_WRA
@@ -1223,17 +1248,9 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
             if (kc + 1 < NC) load_epk(k2 + 1);
           }
         }
-        if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
+        if constexpr (!CONV_DMA_SPREAD) {
 #pragma unroll
-          for (int u = 0; u < PPS; ++u) {
-            const int k = st * PPS + u;
-            if (k < NPER) {
-              if constexpr (NEXT == 3) dma.piece2(nbase, k, nkc - dma.n1, lane);
-              else dma.piece1(nbase, k, nkc, lane);
-            } else if (NEXT == 2 && k < NPC) {
-              dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
-            }
-          }
+          for (int u = 0; u < PPS; ++u) dma_piece(st, u);
         }
         __builtin_amdgcn_sched_barrier(0);
       });
@@ -1458,6 +1475,26 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       constexpr int HALF = 16 * ROWB;
       static_assert(NS % 2 == 0, "B double buffer alternates per step");
       fragT am;
+      // the step's DMA pieces: piece u after MFMA group dma_g(u) of the six (CONV_DMA_SPREAD), else after the step
+      auto dma_piece = [&](int st, int u) {
+        if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
+          const int k = st * PPS + u;
+          if (k < NPER) {
+            if constexpr (NEXT == 3) dma.piece2(nbase, k, nkc - dma.n1, lane);
+            else dma.piece1(nbase, k, nkc, lane);
+          } else if (NEXT == 2 && k < NPC) {
+            dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
+          }
+        }
+      };
+      auto dma_step = [&](auto st_tag, auto g_tag) {
+        constexpr int st = decltype(st_tag)::value, g = decltype(g_tag)::value;
+        if constexpr (CONV_DMA_SPREAD)
+          static_for<0, PPS>([&](auto u_tag) {
+            constexpr int u = decltype(u_tag)::value;
+            if constexpr ((u * 6) / PPS + 1 == g || (g == 5 && (u * 6) / PPS + 1 > 5)) dma_piece(st, u);
+          });
+      };
       static_for<0, NS>([&](auto st_tag) {
         constexpr int st = decltype(st_tag)::value;
         constexpr int j = st, sb = st & 1, pb = sb ^ 1;
@@ -1489,27 +1526,39 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   }
 #define PETDIFF_URB(q, ptr) \
   if constexpr (!(CONV_EXP_MODE & 64)) bv[sb][q] = *reinterpret_cast<const fragT*>(ptr);
+        using G0 = std::integral_constant<int, 0>;
+        using G1 = std::integral_constant<int, 1>;
+        using G2 = std::integral_constant<int, 2>;
+        using G3 = std::integral_constant<int, 3>;
+        using G4 = std::integral_constant<int, 4>;
+        using G5 = std::integral_constant<int, 5>;
         PETDIFF_UMF(0, 0)
         PETDIFF_URB(0, pb0)
+        dma_step(st_tag, G0{});
         __builtin_amdgcn_sched_barrier(0);
         PETDIFF_UMF(0, 1)
         PETDIFF_URB(1, pb0 + HALF)
+        dma_step(st_tag, G1{});
         __builtin_amdgcn_sched_barrier(0);
         PETDIFF_UMF(1, 0)
         PETDIFF_URB(2, pb1)
+        dma_step(st_tag, G2{});
         __builtin_amdgcn_sched_barrier(0);
         PETDIFF_UMF(1, 1)
         PETDIFF_URB(3, pb1 + HALF)
+        dma_step(st_tag, G3{});
         __builtin_amdgcn_sched_barrier(0);
         PETDIFF_UMF(2, 0)
         PETDIFF_URA(0, 0)
         PETDIFF_URA(0, 1)
+        dma_step(st_tag, G4{});
         __builtin_amdgcn_sched_barrier(0);
         PETDIFF_UMF(2, 1)
         PETDIFF_URA(1, 0)
         PETDIFF_URA(1, 1)
         PETDIFF_URA(2, 0)
         PETDIFF_URA(2, 1)
+        dma_step(st_tag, G5{});
 #undef PETDIFF_URB
 #undef PETDIFF_URA
 #undef PETDIFF_UMF
@@ -1526,17 +1575,9 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
             if (kc + 1 < NC) load_epk(k2 + 1);
           }
         }
-        if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
+        if constexpr (!CONV_DMA_SPREAD) {
 #pragma unroll
-          for (int u = 0; u < PPS; ++u) {
-            const int k = st * PPS + u;
-            if (k < NPER) {
-              if constexpr (NEXT == 3) dma.piece2(nbase, k, nkc - dma.n1, lane);
-              else dma.piece1(nbase, k, nkc, lane);
-            } else if (NEXT == 2 && k < NPC) {
-              dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
-            }
-          }
+          for (int u = 0; u < PPS; ++u) dma_piece(st, u);
         }
         __builtin_amdgcn_sched_barrier(0);
       });
