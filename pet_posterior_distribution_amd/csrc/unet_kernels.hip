@@ -29,8 +29,7 @@
 // The fused final level's time / label map rows: 0 = read from L2 by the transposed final conv in the
 // epilogue, 1 = staged in LDS by LDS-DMA at kernel start (54 KB in the start-up burst of all 256
 // workgroups; A/B: 5035-5051 vs 5093 samples/s for 0, profiles/r04/ab_r4d)
-// 16x16x32 fused levels (up0, up1): the step's LDS-DMA pieces issued between its fragment groups' MFMAs
-// (1) or after all of them (0)
+// fused levels: a K step's LDS-DMA pieces issued between its MFMA groups (1) or after all of them (0)
 #ifndef CONV_DMA_SPREAD
 #define CONV_DMA_SPREAD 1
 #endif
@@ -1683,6 +1682,33 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       constexpr int PPS = (NPC + NS - 1) / NS;            // DMA pieces per step
       static_assert(NS % 2 == 0, "fragment double buffer alternates per step");
       fragT am[SEG == 2 ? NH : 1];
+      // DMA piece u of step st after the step's MFMA g = u * 6 / PPS + 1 (CONV_DMA_SPREAD; the last ones after
+      // its sixth), else all after the step
+      auto dma_piece = [&](int st, int u) {
+        if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
+          const int k = st * PPS + u;
+          if (k < NPER) {
+            if constexpr (NEXT == 3) dma.piece2(nbase, k, nkc - dma.n1, lane);
+            else dma.piece1(nbase, k, nkc, lane);
+          } else if (NEXT == 2 && k < NPC) {
+            dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
+          }
+        }
+      };
+      auto dma_at = [&](int st, auto g_tag) {
+        constexpr int g = decltype(g_tag)::value;
+        if constexpr (CONV_DMA_SPREAD && NEXT != 0)
+          static_for<0, PPS>([&](auto u_tag) {
+            constexpr int u = decltype(u_tag)::value;
+            if constexpr ((u * 6) / PPS + 1 == g || (g == 5 && (u * 6) / PPS + 1 > 5)) dma_piece(st, u);
+          });
+      };
+      using D0 = std::integral_constant<int, 0>;
+      using D1 = std::integral_constant<int, 1>;
+      using D2 = std::integral_constant<int, 2>;
+      using D3 = std::integral_constant<int, 3>;
+      using D4 = std::integral_constant<int, 4>;
+      using D5 = std::integral_constant<int, 5>;
 #pragma unroll
       for (int st = 0; st < NS; ++st) {
         const int j = st / NG, g = st % NG, sb = st & 1;
@@ -1707,20 +1733,26 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   if constexpr (!(CONV_EXP_MODE & 64)) dst = *reinterpret_cast<const fragT*>(ptr);
         PETDIFF_MF(0, 0)
         PETDIFF_RD(av[sb][0], pa0)
+        dma_at(st, D0{});
         __builtin_amdgcn_sched_barrier(0);
         PETDIFF_MF(1, 0)
         PETDIFF_RD(bv[sb][0], pb0)
+        dma_at(st, D1{});
         __builtin_amdgcn_sched_barrier(0);
         PETDIFF_MF(2, 0)
         PETDIFF_RD(av[sb][1], pa1)
+        dma_at(st, D2{});
         __builtin_amdgcn_sched_barrier(0);
         PETDIFF_MF(0, 1)
         PETDIFF_RD(av[sb][2], pa2)
+        dma_at(st, D3{});
         __builtin_amdgcn_sched_barrier(0);
         PETDIFF_MF(1, 1)
         PETDIFF_RD(bv[sb][1], pb1)
+        dma_at(st, D4{});
         __builtin_amdgcn_sched_barrier(0);
         PETDIFF_MF(2, 1)
+        dma_at(st, D5{});
 #undef PETDIFF_RD
 #undef PETDIFF_MF
         if constexpr (SEG == 2) {
@@ -1740,17 +1772,9 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
             if (kc + 1 < NC) load_epk(k2 + 1);
           }
         }
-        if constexpr (NEXT != 0 && !(CONV_EXP_MODE & 1)) {
+        if constexpr (!CONV_DMA_SPREAD) {
 #pragma unroll
-          for (int u = 0; u < PPS; ++u) {
-            const int k = st * PPS + u;
-            if (k < NPER) {
-              if constexpr (NEXT == 3) dma.piece2(nbase, k, nkc - dma.n1, lane);
-              else dma.piece1(nbase, k, nkc, lane);
-            } else if (NEXT == 2 && k < NPC) {
-              dma.piece1(nbase + G::STAGE, k - G::PER, nkc + 1, lane);
-            }
-          }
+          for (int u = 0; u < PPS; ++u) dma_piece(st, u);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
