@@ -33,6 +33,11 @@
 #ifndef CONV_DMA_SPREAD
 #define CONV_DMA_SPREAD 1
 #endif
+// the MFMA group (0..5) of a step after which its DMA piece u of pps goes (CONV_DMA_SPREAD): u 6 / pps + CONV_DMA_OFS
+#ifndef CONV_DMA_OFS
+#define CONV_DMA_OFS 1
+#endif
+constexpr int dma_group(int u, int pps) { return (u * 6) / pps + CONV_DMA_OFS < 5 ? (u * 6) / pps + CONV_DMA_OFS : 5; }
 #ifndef CONV_FIN_LDS_MAPS
 #define CONV_FIN_LDS_MAPS 0
 #endif
@@ -1177,7 +1182,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         constexpr int st = decltype(st_tag)::value, g = decltype(g_tag)::value;
         static_for<0, PPS>([&](auto u_tag) {
           constexpr int u = decltype(u_tag)::value;
-          if constexpr ((u * 6) / PPS + 1 == g || (g == 5 && (u * 6) / PPS + 1 > 5)) dma_piece(st, u);
+          if constexpr (dma_group(u, PPS) == g) dma_piece(st, u);
         });
       };
       static_for<0, NS>([&](auto st_tag) {
@@ -1491,7 +1496,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         if constexpr (CONV_DMA_SPREAD)
           static_for<0, PPS>([&](auto u_tag) {
             constexpr int u = decltype(u_tag)::value;
-            if constexpr ((u * 6) / PPS + 1 == g || (g == 5 && (u * 6) / PPS + 1 > 5)) dma_piece(st, u);
+            if constexpr (dma_group(u, PPS) == g) dma_piece(st, u);
           });
       };
       static_for<0, NS>([&](auto st_tag) {
@@ -1700,7 +1705,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         if constexpr (CONV_DMA_SPREAD && NEXT != 0)
           static_for<0, PPS>([&](auto u_tag) {
             constexpr int u = decltype(u_tag)::value;
-            if constexpr ((u * 6) / PPS + 1 == g || (g == 5 && (u * 6) / PPS + 1 > 5)) dma_piece(st, u);
+            if constexpr (dma_group(u, PPS) == g) dma_piece(st, u);
           });
       };
       using D0 = std::integral_constant<int, 0>;
