@@ -10,7 +10,8 @@
 //
 // Design: activations are channels-last rows [sample*L + l][C] in
 // HBM.  Every x-dependent Conv1D is an implicit GEMM  M = B*L, N = Cout,
-// K = taps*Cin  on MFMA (bf16 32x32x16 or exact-f32 32x32x2).  A workgroup owns
+// K = taps*Cin  on MFMA (bf16 / fp16 16x16x32 on down2, down3, up0.fused, up1.fused (M16 in conv_body),
+// 32x32x16 on down1 and the final level, exact-f32 32x32x2).  A workgroup owns
 // 192 rows = whole samples, so the 'same'-padding halo of all taps is served
 // from ONE LDS copy of the input rows (tap j = row shift, out-of-range rows read
 // a zero row).  The label / time channels of every concat are constant per
@@ -26,9 +27,6 @@
 #ifndef CONV_LOADERS
 #define CONV_LOADERS 1
 #endif
-// The fused final level's time / label map rows: 0 = read from L2 by the transposed final conv in the
-// epilogue, 1 = staged in LDS by LDS-DMA at kernel start (54 KB in the start-up burst of all 256
-// workgroups; A/B: 5035-5051 vs 5093 samples/s for 0, profiles/r04/ab_r4d)
 // fused levels: a K step's LDS-DMA pieces issued between its MFMA groups (1) or after all of them (0)
 #ifndef CONV_DMA_SPREAD
 #define CONV_DMA_SPREAD 1
@@ -38,6 +36,9 @@
 #define CONV_DMA_OFS 1
 #endif
 constexpr int dma_group(int u, int pps) { return (u * 6) / pps + CONV_DMA_OFS < 5 ? (u * 6) / pps + CONV_DMA_OFS : 5; }
+// The fused final level's time / label map rows: 0 = read from L2 by the transposed final conv in the
+// epilogue, 1 = staged in LDS by LDS-DMA at kernel start (54 KB in the start-up burst of all 256
+// workgroups; A/B: 5035-5051 vs 5093 samples/s for 0, profiles/r04/ab_r4d)
 #ifndef CONV_FIN_LDS_MAPS
 #define CONV_FIN_LDS_MAPS 0
 #endif
@@ -66,7 +67,8 @@ constexpr int dma_group(int u, int pps) { return (u * 6) / pps + CONV_DMA_OFS < 
 //    tap) MFMA is wholly useful or wholly SAME padding; the zero ones are dropped at compile time.  Wave w
 //    computes fragment set w >> 1 (down3: the 6 positions of sample half w >> 1; down2: positions
 //    {0,2,3,10,4,5} / {1,9,6,11,7,8}) for output columns [32 (w & 1), +32): one B read per 6 MFMAs, and
-//    each input position the set's taps read is loaded from LDS once per k-group (zap[half][position]).
+//    each input position the set's taps read is loaded from LDS once per k-group (zap[half][position];
+//    on 16x16x32: once per tap step, zap[row half][position]).
 //  * up0.fused, the same idea on the coarse rows: wave w computes output phase w >> 1, all 6 coarse rows,
 //    for columns [32 (w & 1), +32), zero products skipped, A cached per input position.
 //  * up1.fused (16 samples per tile, a fragment is coarse rows m, m + 1): the A fragment of (i, j) equals
