@@ -31,11 +31,15 @@
 #ifndef CONV_DMA_SPREAD
 #define CONV_DMA_SPREAD 1
 #endif
-// the MFMA group (0..5) of a step after which its DMA piece u of pps goes (CONV_DMA_SPREAD): u 6 / pps + CONV_DMA_OFS
+// the MFMA group (0..5) of a step after which its DMA piece u of pps goes (CONV_DMA_SPREAD): u 6 / pps + ofs, ofs =
+// CONV_DMA_OFS (-1: per layer, 1 on up1.fused and 2 on the others, the better of 1 / 2 in profiles/r04/r4aa_dma_ofs)
 #ifndef CONV_DMA_OFS
-#define CONV_DMA_OFS 1
+#define CONV_DMA_OFS -1
 #endif
-constexpr int dma_group(int u, int pps) { return (u * 6) / pps + CONV_DMA_OFS < 5 ? (u * 6) / pps + CONV_DMA_OFS : 5; }
+constexpr int dma_group(int u, int pps, int kind) {
+  const int ofs = CONV_DMA_OFS >= 0 ? CONV_DMA_OFS : kind == petdiff::LK_UP1_F ? 1 : 2;
+  return (u * 6) / pps + ofs < 5 ? (u * 6) / pps + ofs : 5;
+}
 // The fused final level's time / label map rows: 0 = read from L2 by the transposed final conv in the
 // epilogue, 1 = staged in LDS by LDS-DMA at kernel start (54 KB in the start-up burst of all 256
 // workgroups; A/B: 5035-5051 vs 5093 samples/s for 0, profiles/r04/ab_r4d)
@@ -1184,7 +1188,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         constexpr int st = decltype(st_tag)::value, g = decltype(g_tag)::value;
         static_for<0, PPS>([&](auto u_tag) {
           constexpr int u = decltype(u_tag)::value;
-          if constexpr (dma_group(u, PPS) == g) dma_piece(st, u);
+          if constexpr (dma_group(u, PPS, KIND) == g) dma_piece(st, u);
         });
       };
       static_for<0, NS>([&](auto st_tag) {
@@ -1498,7 +1502,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         if constexpr (CONV_DMA_SPREAD)
           static_for<0, PPS>([&](auto u_tag) {
             constexpr int u = decltype(u_tag)::value;
-            if constexpr (dma_group(u, PPS) == g) dma_piece(st, u);
+            if constexpr (dma_group(u, PPS, KIND) == g) dma_piece(st, u);
           });
       };
       static_for<0, NS>([&](auto st_tag) {
@@ -1707,7 +1711,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         if constexpr (CONV_DMA_SPREAD && NEXT != 0)
           static_for<0, PPS>([&](auto u_tag) {
             constexpr int u = decltype(u_tag)::value;
-            if constexpr (dma_group(u, PPS) == g) dma_piece(st, u);
+            if constexpr (dma_group(u, PPS, KIND) == g) dma_piece(st, u);
           });
       };
       using D0 = std::integral_constant<int, 0>;
