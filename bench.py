@@ -650,6 +650,17 @@ def mh_config2_and_protocol(iddpm_10k_s, dev, cpu=True):
     torch.cuda.synchronize()
     proto = (time.perf_counter() - t1) * 10
     mh.close()
+    # the paper's own comparison (README.md:12): the network on the GPU against MCMC on CPU cores.  PyMC runs
+    # its 4 chains in parallel processes, so the protocol takes one chain's 60k steps on 4 cores; here the
+    # C restatement of the same sampler (oracle/mh_ref.c, 4 OpenMP threads, one chain each), timed on
+    # 4 x (2000 + 4000) steps and scaled x 10 (about 1 s of CPU work)
+    cpu_proto = None
+    if cpu:
+        from oracle import mh_c
+        prob = mh_c.MHProblem(**P)
+        t2 = time.perf_counter()
+        prob.run(4, 2000, 4000, seed=3, threads=4)
+        cpu_proto = (time.perf_counter() - t2) * 10
     cfg2 = {'value': round(steps / el, 1), 'unit': 'chain-steps/s', 'chains': n, 'steps_per_chain': tune + draws,
             'tune': tune, 'draws': draws, 'seconds': round(el, 3), 'dtype': 'f64',
             'roofline': {'bound': 'valu-fp64', 'achieved': round(fl, 2), 'peak': 78.6, 'unit': 'TFLOP/s',
@@ -660,7 +671,11 @@ def mh_config2_and_protocol(iddpm_10k_s, dev, cpu=True):
             {'mh_protocol_s_per_tac': round(proto, 3), 'mh_protocol': '4 chains x (20000 draws + 40000 tune), '
              'timed as 4 x (2000 + 4000) x 10', 'iddpm_s_per_tac': round(iddpm_10k_s, 3),
              'iddpm_protocol': '10,000 posterior samples x 1000 reverse steps, bf16, one launch',
-             'iddpm_speedup_over_mh': round(proto / iddpm_10k_s, 2), 'reference_claim': '> 230x (README.md:12)'})
+             'iddpm_speedup_over_mh': round(proto / iddpm_10k_s, 2), 'reference_claim': '> 230x (README.md:12)',
+             'mh_cpu_protocol_s_per_tac': None if cpu_proto is None else round(cpu_proto, 3),
+             'mh_cpu_protocol': 'oracle/mh_ref.c (gcc -O3, OpenMP), 4 threads = one chain each, as PyMC runs its '
+                                '4 chains; 4 x (2000 + 4000) steps timed, x 10',
+             'iddpm_gpu_over_mh_cpu': None if cpu_proto is None else round(cpu_proto / iddpm_10k_s, 2)})
 
 
 def weights_sensitivity(net, cond, B, dev, reps=3):
@@ -744,7 +759,7 @@ def main():
     # r * B .. r * B + B - 1; x_T and z from the counter-based Philox stream keyed by the global sample index.
     # One bench step = one whole job: x_T, the 1000-step generate (one replayed hipGraph per launch of
     # <= PETDIFF_MAX_BATCH samples), the GPU Welford statistics and their all-gather + merge.
-    from pet_posterior_distribution_amd.distributed import TacTable, sample_posterior_sharded
+    from pet_posterior_distribution_amd.distributed import TacTable, sample_posterior_sharded, rank_tac_range
     n_per = B // n_tac
     table = TacTable(world * n_tac, lambda k: make_condition(seed=k))
     cond = table.rows(range(rank * n_tac, rank * n_tac + n_tac))          # this rank's TACs (built once)
@@ -782,10 +797,11 @@ def main():
     _, allst, (lo, hi, out) = res
     assert (lo, hi) == (offset, offset + B)
     if world > 1:                              # the all-gather alone, timed once after the loop
-        from pet_posterior_distribution_amd.distributed import allgather_stats
+        from pet_posterior_distribution_amd.distributed import gather_merge_own_tacs, rank_tac_range
+        t0r, t1r = rank_tac_range(len(allst), n_per, world, rank)
         torch.cuda.synchronize()
         ta = time.perf_counter()
-        allgather_stats(allst, device=coll)
+        gather_merge_own_tacs(allst[t0r:t1r], len(allst), n_per, device=coll)
         torch.cuda.synchronize()
         ag['ms'] = (time.perf_counter() - ta) * 1e3
     ag_ms = ag['ms']
@@ -825,6 +841,9 @@ def main():
             'roofline': roof,
             'outputs_finite': finite,
             'stats_allgather_ms': round(ag_ms, 3),
+            # bytes each rank receives: world x the largest rank's TAC range x 2,304 B (own TACs only)
+            'stats_allgather_bytes': world * max(t1 - t0 for t0, t1 in (rank_tac_range(world * n_tac, n_per, world, r)
+                                                                        for r in range(world))) * 48 * 2 * 3 * 8,
         }
         if layer_ms is not None:
             line['layer_us'] = layer_us(layer_ms)

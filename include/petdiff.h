@@ -207,6 +207,12 @@ int petdiff_get_timing(petdiff_handle h, float* total_ms, int* count);
 
 const char* petdiff_last_error(void);
 
+/* Diagnostic (no reference counterpart): the XOR key of 16-B piece slots in an LDS row / packed weight
+ * row that the kernels and the host weight packer share (petdiff_internal.h piece_key): row index, pieces
+ * per row (2, 4 or 8), m16 = 1 for the 16x16x32 layers' 16-row key.  Exported so the CPU tests check the
+ * bank-conflict model against the library's own formula. */
+int petdiff_piece_key(int row, int cpr, int m16);
+
 #ifdef __cplusplus
 }
 #endif

@@ -43,6 +43,7 @@ SYMBOLS = [
     ('petdiff_create', C.c_int, [C.POINTER(PetdiffConfig), C.c_void_p, C.c_size_t, C.c_int, C.POINTER(C.c_void_p)]),
     ('petdiff_destroy', C.c_int, [C.c_void_p]),
     ('petdiff_set_schedule', C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    ('petdiff_piece_key', C.c_int, [C.c_int, C.c_int, C.c_int]),
     ('petdiff_cosine_schedule', C.c_int, [C.c_int, C.c_double, C.c_double, C.c_void_p]),
     ('petdiff_set_conditions', C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
     ('petdiff_forward', C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,

@@ -152,7 +152,6 @@ struct petdiff_ctx {
   // run the next step's down0 inside the previous step's up2.block epilogue (generate);
   // PETDIFF_FUSE_DOWN0=0 restores the standalone down0 launch per step (A/B switch)
   bool fuse_down0 = true;
-  bool up2_x3_paired = true;         // bf16x3: the final level on paired 64-B chunks (LK_UP2_FX3)
   DevBuf xa, xb, tacbuf, tbuf, rng;
   hipStream_t cap_stream = nullptr;
   int seg_steps = 0;                   // reverse steps per captured graph segment (0: the whole loop)
@@ -274,8 +273,7 @@ const FusedLevel kFused[3] = {
 };
 
 // kernel kind of fused level u (the bf16x3 network's final level runs its paired-chunk instance)
-// (PETDIFF_UP2_X3_PAIRED=0: the three-pass 32-B-row instance, an A/B switch read at create)
-int fused_kind(const petdiff_ctx* h, int u) { return (u == 2 && h->x3 && h->up2_x3_paired) ? LK_UP2_FX3 : kFused[u].kind; }
+int fused_kind(const petdiff_ctx* h, int u) { return (u == 2 && h->x3) ? LK_UP2_FX3 : kFused[u].kind; }
 
 // Weights of a fused up level: per N tile, the block's skip-half chunks [6 taps][NT][ROWB]
 // (residual folded into tap 2) then the coarse-input chunks [phase][4 taps][NT][ROWB] of the
@@ -663,7 +661,6 @@ int petdiff_create(const petdiff_config* cfg, const float* weights, size_t n_wei
   h->x3 = cfg->dtype == PETDIFF_DTYPE_BF16X3;
   h->spec = make_spec(*cfg, h->n_out);
   if (const char* e = std::getenv("PETDIFF_FUSE_DOWN0")) h->fuse_down0 = std::atoi(e) != 0;
-  if (const char* e = std::getenv("PETDIFF_UP2_X3_PAIRED")) h->up2_x3_paired = std::atoi(e) != 0;
   h->fuse_up = cfg->dtype != PETDIFF_DTYPE_F32;
   if (const char* e = std::getenv("PETDIFF_FUSE_UP")) h->fuse_up = h->fuse_up && std::atoi(e) != 0;
   const size_t need = h->spec.back().off + h->spec.back().size;
@@ -975,6 +972,8 @@ int petdiff_get_activation(petdiff_handle h, int level, float* out, int B, void*
   else HIPC(launch_to_f32<float>(static_cast<const float*>(src), n, out, s));
   return PETDIFF_OK;
 }
+
+int petdiff_piece_key(int row, int cpr, int m16) { return piece_key(row, cpr, m16 != 0); }
 
 int petdiff_set_timing(petdiff_handle h, int enable) {
   CHK(valid_handle(h));

@@ -161,14 +161,16 @@ constexpr int layer_ntile(int kind) { return 64 * layer_tile(kind).wn; }
 #ifndef CONV_M16
 #define CONV_M16 1
 #endif
-// bf16x3 on the 16x16x32 layers (down2, down3, up0.fused, up1.fused; unet_kernels.hip M16): their chunks walk
-// the three passes (a_hi w_hi, a_hi w_lo, a_lo w_hi) of plain 64-B rows, one k = 32 MFMA step per pass and tap,
-// instead of paired [hi | lo] rows (0: paired chunks on 32x32x16 for every 64-B-row layer)
+// bf16x3 on the 16x16x32 layers (down2, down3, up0.fused, up1.fused; unet_kernels.hip M16 / PX):
+//   2: paired [hi | lo] chunks, two at a time -- units CX, HH, CY of full k = 32 MFMAs (conv_body PX), each
+//      hi / lo byte staged once;
+//   1: three passes (a_hi w_hi, a_hi w_lo, a_lo w_hi) of plain 64-B rows, a_hi and w_hi staged twice.
 #ifndef CONV_M16_X3
-#define CONV_M16_X3 1
+#define CONV_M16_X3 2
 #endif
+static_assert(CONV_M16_X3 == 1 || CONV_M16_X3 == 2, "CONV_M16_X3: 1 three passes, 2 paired units");
 constexpr bool m16_kind(int kind) { return kind == LK_DOWN2 || kind == LK_DOWN3 || kind == LK_UP0_F || kind == LK_UP1_F; }
-constexpr bool x3_paired(int kind) { return layer_tile(kind).rowb == 64 && !(CONV_M16_X3 && m16_kind(kind)); }
+constexpr bool x3_paired(int kind) { return layer_tile(kind).rowb == 64 && !(CONV_M16_X3 == 1 && m16_kind(kind)); }
 // XOR key of 16-B piece index p within a row (an A row in LDS, a packed weight row n): conflict-free ds_read_b128
 // for the lane groups of MI355X_MICROARCH.md's LDS table.  32x32x16 reads 16 rows of one piece per lane group:
 // (row >> 2) & 3.  The 16x16x32 layers (m16: CONV_M16, 16-bit, m16_kind) read 16 rows x 4 pieces per

@@ -902,9 +902,15 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   // 16x16x32 K loop (see mfma16): the position-major layers, 16-bit, not bf16x3
   constexpr bool UC = G::FUSED && G::S == 16 && sizeof(T) == 2 && G::STAGES == 3;   // up1: A cache by key
   // (down1's generic row path on 16x16x32 measured slower: 14.2 vs 13.3 us, at 256 VGPRs; it stays on 32x32x16)
-  constexpr bool M16 = CONV_M16 && sizeof(T) == 2 && (XS == 0 || (CONV_M16_X3 && !P3)) && (G::PM || G::W6 || UC);
-  static_assert(!(G::PM || G::W6 || UC) || sizeof(T) != 2 || M16 == (CONV_M16 && (XS == 0 || CONV_M16_X3)),
+  constexpr bool M16 = CONV_M16 && sizeof(T) == 2 && (G::PM || G::W6 || UC);
+  static_assert(!(G::PM || G::W6 || UC) || sizeof(T) != 2 || M16 == (bool)CONV_M16,
                 "the host packs bf16x3 weights of these layers by m16_kind (petdiff_internal.h)");
+  // PX: bf16x3 on a 16x16x32 layer with paired [hi | lo] chunks (CONV_M16_X3 = 2).  Chunks X = 2 c and
+  // Y = 2 c + 1 (16 channels each) run three units of full k = 32 MFMAs: CX = a_hi(X) w_lo(X) + a_lo(X) w_hi(X)
+  // (B read with its halves swapped), HH = a_hi(X) w_hi(X) + a_hi(Y) w_hi(Y) (lanes 32-63 read Y's hi half
+  // from Y's stage), CY as CX on Y.  Every hi / lo byte is staged once (2 x the bf16 chunks, not 3 x).
+  constexpr bool PX = M16 && P3;
+  static_assert(!P3 || !(G::PM || G::W6 || UC) || !CONV_M16 || PX, "paired bf16x3 on the 16x16x32 layers");
   const int NC = P3 ? (a.c1 + a.c2) / (G::KC / 2) : (XS ? 3 : 1) * (a.c1 / G::KC + a.c2 / G::KC);
 
   // Final level: this thread's output row (one per thread) and every global operand of its
@@ -1070,6 +1076,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
 
   DmaPlan<T, KIND, XS> dma;
   dma.init(a, m0, n_tile, NC, wv, lane);
+  const int U2 = PX && G::FUSED ? 3 * (NC - dma.n1) / 2 : 0;   // PX: segment-2 units
 
   // One chunk: TAPS x (ROWB/32 bf16 | ROWB/64 f32) MFMA steps.  The DMA pieces of
   // chunk nkc (into stage nbuf) are issued spread over the steps (NEXT = false: none).
@@ -1133,8 +1140,23 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
             ((size_t)n_tile * n2 * 2 * NT + (size_t)ph * NT + (G::W6 ? (wv & 1) * 32 : wn * 64) + (M16 ? (lane & 15) : lr)) * ROWB +
             (M16 ? (lane >> 4) : h) * 16;
   }
-  auto load_epk = [&](int kc2) {   // segment-2 chunk kc2's correction fragments
-    if constexpr (G::FUSED && M16) {   // epk[ch][jn]: column half ch of fragment jn, the whole 64-B row
+  auto load_epk = [&](int kc2) {   // segment-2 chunk kc2's correction fragments (PX: segment-2 unit kc2)
+    if constexpr (G::FUSED && PX) {
+      // unit v = 3 c + t of pair c (chunks X = 2 c, Y = 2 c + 1): CX / CY read the chunk's row with its
+      // halves swapped ([w_lo | w_hi]); HH reads X's hi half (lanes 0-31) and Y's hi half (lanes 32-63)
+      const int c = kc2 / 3, t = kc2 - 3 * c;
+      const bool lo_lanes = (lane & 32) == 0;
+      const int k = (t == 0 || (t == 1 && lo_lanes)) ? 2 * c : 2 * c + 1;
+      // the other 32-B half of the lane's 64-B row: piece (lane >> 4) ^ 2, as pointer arithmetic (an integer
+      // XOR of the address would lose the global address space: flat loads, and vmcnt(0) waits on the ring)
+      const int sw = (t == 1 && lo_lanes) ? 0 : (lane & 32) ? -32 : 32;
+      const char* p = ebase + (size_t)k * 2 * NT * ROWB + sw;
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+        for (int jn = 0; jn < (G::W6 ? 1 : 2); ++jn)
+          epk[ch][jn] = *reinterpret_cast<const fragT*>(p + jn * 32 * ROWB + ch * 16 * ROWB);
+    } else if constexpr (G::FUSED && M16) {   // epk[ch][jn]: column half ch of fragment jn, the whole 64-B row
       const char* p = ebase + (size_t)kc2 * 2 * NT * ROWB;
 #pragma unroll
       for (int ch = 0; ch < 2; ++ch)
@@ -1151,12 +1173,24 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   };
   // NEXT = 2 (first chunk only): the pieces of chunks nkc and nkc + 1 (stages nbuf, nbuf + 1).
   // SEG = 2: a fused segment-2 chunk (4 composite taps of this wave's phase; kc = its index).
-  auto compute = [&](const char* base, auto next_tag, int nkc, int nbuf, auto seg_tag, int kc, auto pat_tag) {
+  // unit_tag (PX only): 0 a plain chunk, 1 a cross unit (CX / CY: B halves swapped), 2 the hi-hi unit HH, whose
+  // lanes 32-63 read the Y chunk's hi half at base + dst (dst: Y's stage minus X's, bytes)
+  auto compute_u = [&](const char* base, auto next_tag, int nkc, int nbuf, auto seg_tag, int kc, auto pat_tag,
+                       auto unit_tag, int dst) {
     constexpr int NEXT = (int)decltype(next_tag)::value;
     // SEG: 1 / 2; seg_tag 4 = the first segment-2 chunk (up0 zero-skip: its step 0 carries segment 1's last step)
     constexpr int SEGV = (int)decltype(seg_tag)::value;
     constexpr int SEG = SEGV == 4 ? 2 : SEGV;
     char* nbase = smem + nbuf * G::STAGE;
+    // A / B fragment reads of the M16 paths: ab + (offset ^ AX), ab + ((offset ^ BX) + tap row)
+    constexpr int UT = (int)decltype(unit_tag)::value;
+    static_assert(UT == 0 || PX, "units: paired bf16x3 on 16x16x32 only");
+    const char* ab = base;
+    int AX = 0, BX = UT == 1 ? 32 : 0;
+    if constexpr (UT == 2) {
+      ab = base + ((lane & 32) ? dst : 0);
+      AX = BX = lane & 32;
+    }
     if constexpr (G::W6 && M16) {
       // up0.fused on 16x16x32: step st = tap zs_tap(jj) (one k = 32 step per tap); reads: the step's two B
       // column halves, then both row halves of the positions first needed at this tap; MFMAs of step st - 1:
@@ -1196,7 +1230,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         constexpr int jj = st, sb = st & 1, pb = sb ^ 1;
         constexpr int j = G::zs_tap(SEG, jj);
         constexpr int jpp = G::zs_tap(SEG, st == 0 ? NS - 1 : st - 1);
-        const char* pb0 = base + (SEG == 2 ? boff2[0] : boff[0]) + j * NT * ROWB;
+        const char* pb0 = ab + (((SEG == 2 ? boff2[0] : boff[0]) ^ BX) + j * NT * ROWB);
         auto body = [&](auto prev_tag) {
           constexpr int PV = decltype(prev_tag)::value;   // 0: this segment's step st - 1; 1 / 2: segment 1's / 2's last
           constexpr int SP = PV == 0 ? SEG : PV;
@@ -1212,9 +1246,9 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
 #define PETDIFF_WRA(f)                                                                                      \
   if constexpr (G::w6_ok(SEG, PAT, f, j) && G::w6_first(SEG, PAT, f, jj) && !(CONV_EXP_MODE & 64)) {        \
     constexpr int P_ = G::w6_pos(SEG, PAT, f, j);                                                            \
-    const int ao_ = SEG == 2 ? apos2[P_ < G::LH ? P_ : 0] : apos1[P_];                                       \
-    zap[0][P_] = *reinterpret_cast<const fragT*>(base + ao_);                                                \
-    zap[1][P_] = *reinterpret_cast<const fragT*>(base + ao_ + HALF);                                         \
+    const int ao_ = (SEG == 2 ? apos2[P_ < G::LH ? P_ : 0] : apos1[P_]) ^ AX;                                \
+    zap[0][P_] = *reinterpret_cast<const fragT*>(ab + ao_);                                                  \
+    zap[1][P_] = *reinterpret_cast<const fragT*>(ab + ao_ + HALF);                                           \
   }
           // fragment f's reads go after fragment min(f + 2, 5)'s MFMAs, and after the last MFMA of the step
           // that still multiplies the zap entry they replace (both row halves of a position share a slot)
@@ -1244,8 +1278,8 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         else body(std::integral_constant<int, 2>{});
         if constexpr (SEG == 2) {
           if (st == 0) {
-            am[0] = *reinterpret_cast<const fragT*>(base + amask);
-            am[1] = *reinterpret_cast<const fragT*>(base + amask + HALF);
+            am[0] = *reinterpret_cast<const fragT*>(ab + (amask ^ AX));
+            am[1] = *reinterpret_cast<const fragT*>(ab + (amask ^ AX) + HALF);
           }
           if (st == 1) {
             if constexpr (!(CONV_EXP_MODE & 2)) {
@@ -1254,8 +1288,12 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
               mfma16_blk<2>(acc[0][0], am[1], epk[0][0]);
               mfma16_blk<3>(acc[0][0], am[1], epk[1][0]);
             }
-            const int k2 = kc - dma.n1;
-            if (kc + 1 < NC) load_epk(k2 + 1);
+            if constexpr (PX) {
+              if (kc + 1 < U2) load_epk(kc + 1);
+            } else {
+              const int k2 = kc - dma.n1;
+              if (kc + 1 < NC) load_epk(k2 + 1);
+            }
           }
         }
         if constexpr (!CONV_DMA_SPREAD) {
@@ -1368,14 +1406,14 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         constexpr int st = decltype(st_tag)::value;
         constexpr int j = st, sb = st & 1, pb = sb ^ 1;
         constexpr int jp = st == 0 ? TAPS - 1 : st - 1;
-        const char* pb0 = base + boff[0] + j * NT * ROWB;
+        const char* pb0 = ab + ((boff[0] ^ BX) + j * NT * ROWB);
 #define PETDIFF_QMF(f, rh, ch)                                                                              \
   if constexpr (G::pw6_valid(SET, f, jp) && !(CONV_EXP_MODE & 2))                                           \
     mfma16_blk<2 * (rh) + (ch)>(acc[(f) % 3][(f) / 3], zap[rh][G::pw6_pos(SET, f) + jp - PADL], bv[pb][ch]);
 #define PETDIFF_QRA(f, rh)                                                                                  \
   if constexpr (G::pw6_valid(SET, f, j) && G::pw6_first(SET, f, j) && !(CONV_EXP_MODE & 64)) {              \
     constexpr int P_ = G::pw6_pos(SET, f) + j - PADL;                                                        \
-    zap[rh][P_] = *reinterpret_cast<const fragT*>(base + apm[P_] + (rh) * HALF);                             \
+    zap[rh][P_] = *reinterpret_cast<const fragT*>(ab + (apm[P_] ^ AX) + (rh) * HALF);                        \
   }
 #define PETDIFF_QF(f)                                                                                       \
   PETDIFF_QMF(f, 0, 0)                                                                                      \
@@ -1511,8 +1549,8 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         constexpr bool PS1 = st > 0 ? SEG == 1 : (SEG == 1 || SEGV == 4);   // the previous step's segment is 1
         constexpr int KSP = PS1 ? 4 : 2, HKP = KSP / 2;
         constexpr int JP = st > 0 ? st - 1 : PS1 ? TAPS - 1 : G::TAPS2 - 1;
-        const char* pb0 = base + (SEG == 2 ? boff2[0] : boff[0]) + j * NT * ROWB;
-        const char* pb1 = base + (SEG == 2 ? boff2[1] : boff[1]) + j * NT * ROWB;
+        const char* pb0 = ab + (((SEG == 2 ? boff2[0] : boff[0]) ^ BX) + j * NT * ROWB);
+        const char* pb1 = ab + (((SEG == 2 ? boff2[1] : boff[1]) ^ BX) + j * NT * ROWB);
         // (i, rh) first reads key KS i + HK rh + j unless an earlier tap of this chunk read it
         auto first = [](int i, int rh) {
           for (int j2 = 0; j2 < j; ++j2)
@@ -1532,7 +1570,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
 #define PETDIFF_URA(i, rh)                                                                                  \
   if constexpr (first(i, rh) && !(CONV_EXP_MODE & 64)) {                                                    \
     constexpr int K_ = KS * (i) + HK * (rh) + j;                                                             \
-    ucm[K_] = *reinterpret_cast<const fragT*>(base + (SEG == 2 ? akey2[K_] : akey1[K_]));                    \
+    ucm[K_] = *reinterpret_cast<const fragT*>(ab + ((SEG == 2 ? akey2[K_] : akey1[K_]) ^ AX));               \
   }
 #define PETDIFF_URB(q, ptr) \
   if constexpr (!(CONV_EXP_MODE & 64)) bv[sb][q] = *reinterpret_cast<const fragT*>(ptr);
@@ -1573,7 +1611,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
 #undef PETDIFF_URA
 #undef PETDIFF_UMF
         if constexpr (SEG == 2) {
-          if (st == 0 && has_m0) am = *reinterpret_cast<const fragT*>(base + amask);
+          if (st == 0 && has_m0) am = *reinterpret_cast<const fragT*>(ab + (amask ^ AX));
           if (st == 1 && has_m0) {
             if constexpr (!(CONV_EXP_MODE & 2)) {
               mfma16_blk<0>(acc[0][0], am, epk[0][0]);
@@ -1581,8 +1619,12 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
               mfma16_blk<0>(acc[0][1], am, epk[0][1]);
               mfma16_blk<1>(acc[0][1], am, epk[1][1]);
             }
-            const int k2 = kc - dma.n1;
-            if (kc + 1 < NC) load_epk(k2 + 1);
+            if constexpr (PX) {
+              if (kc + 1 < U2) load_epk(kc + 1);
+            } else {
+              const int k2 = kc - dma.n1;
+              if (kc + 1 < NC) load_epk(k2 + 1);
+            }
           }
         }
         if constexpr (!CONV_DMA_SPREAD) {
@@ -1833,6 +1875,11 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       }
     }
   };
+  auto compute = [&](const char* base, auto next_tag, int nkc, int nbuf, auto seg_tag, int kc, auto pat_tag) {
+    compute_u(base, next_tag, nkc, nbuf, seg_tag, kc, pat_tag, std::integral_constant<int, 0>{}, 0);
+  };
+  using UCross = std::integral_constant<int, 1>;   // PX units
+  using UHiHi = std::integral_constant<int, 2>;
   using Yes = std::integral_constant<int, 1>;
   using No = std::integral_constant<int, 0>;
   using Two = std::integral_constant<int, 2>;
@@ -1981,6 +2028,41 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       st_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
       auto fused_loop = [&](auto pat_tag) {
+       if constexpr (PX) {
+        // paired bf16x3 units (PX): pair c = chunks X_c = 2 c (stage sx), Y_c = 2 c + 1 (stage sx + 1 mod 3).
+        // CX(c) issues X_{c+1} into the stage Y_{c-1} left, CY(c) issues Y_{c+1} into X_c's stage (free after
+        // HH(c)); X_c lands 3 units after its issue, Y_c 2 units.  Pairs [0, P1) are segment 1, [P1, P)
+        // segment 2 (host: P1 >= 2, P - P1 >= 2); segment-2 unit v = 3 (c - P1) + t picks the correction
+        // weights (load_epk).
+        const int P1 = n1 / 2, P = NC / 2;
+        int sx = 2;
+        auto px_pair = [&](int c, auto seg_tag, auto next_tag, auto wait_tag, int v0) {
+          constexpr int W = decltype(wait_tag)::value;
+          constexpr int SR = decltype(seg_tag)::value == 4 ? 2 : decltype(seg_tag)::value;
+          using SegR = std::integral_constant<int, SR>;
+          const int sy = sx == 2 ? 0 : sx + 1, sxn = sx == 0 ? 2 : sx - 1;
+          compute_u(smem + sx * G::STAGE, next_tag, 2 * c + 2, sxn, seg_tag, v0, pat_tag, UCross{}, 0);
+          ring_barrier<W>();
+          compute_u(smem + sx * G::STAGE, No{}, 0, 0, SegR{}, v0 + 1, pat_tag, UHiHi{}, (sy - sx) * G::STAGE);
+          ring_barrier<W>();
+          compute_u(smem + sy * G::STAGE, next_tag, 2 * c + 3, sx, SegR{}, v0 + 2, pat_tag, UCross{}, 0);
+          ring_barrier<W>();
+          sx = sxn;
+        };
+        // pair 0: CX(0) issues Y_0 (chunk 1 -> stage 1) and X_1 (chunk 2 -> stage 2); CY(0) Y_1 -> stage 0
+        compute_u(smem, Two{}, 1, 1, Seg1{}, 0, pat_tag, UCross{}, 0);
+        ring_barrier<G::PER>();
+        compute_u(smem, No{}, 0, 0, Seg1{}, 0, pat_tag, UHiHi{}, G::STAGE);
+        ring_barrier<G::PER>();
+        compute_u(smem + G::STAGE, Yes{}, 3, 0, Seg1{}, 0, pat_tag, UCross{}, 0);
+        ring_barrier<G::PER>();
+        int c = 1;
+        for (; c + 1 < P1; ++c) px_pair(c, Seg1{}, Yes{}, std::integral_constant<int, G::PER>{}, 0);
+        px_pair(c++, Seg1{}, Seg2Next{}, std::integral_constant<int, G::PER2>{}, 0);   // the next pair: segment 2
+        px_pair(c++, Seg2First{}, Seg2Next{}, std::integral_constant<int, G::PER2>{}, 0);
+        for (; c + 1 < P; ++c) px_pair(c, Seg2{}, Seg2Next{}, std::integral_constant<int, G::PER2>{}, 3 * (c - P1));
+        px_pair(c, Seg2{}, No{}, std::integral_constant<int, 0>{}, 3 * (c - P1));
+       } else {
         compute(smem, Two{}, 1, 1, Seg1{}, 0, pat_tag);              // chunks 1, 2 -> stages 1, 2
         ring_barrier<G::PER>();
         int buf = 1, kc = 1;
@@ -2010,6 +2092,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         buf = buf == 2 ? 0 : buf + 1;
         compute(smem + buf * G::STAGE, No{}, 0, 0, Seg2{}, kc + 1, pat_tag);
         ring_barrier<0>();
+       }
         if constexpr (G::W6 && M16) {   // the last chunk's last step (composite tap 3), four blocks a fragment
           constexpr int PAT = decltype(pat_tag)::value;
           static_for<0, 6>([&](auto f_tag) {
@@ -2063,7 +2146,29 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   if constexpr (G::LDR) {
     // Loader waves: chunk c lands in stage c % 3; barrier B(c+1) closes the MFMA waves'
     // work on chunk c, after which stage c % 3 takes chunk c + 3.
-    if (loader) {
+    if (loader && PX) {
+      // paired bf16x3 units (PX, see fused_loop): X_c = chunk 2 c in stage sx = -c mod 3, Y_c = 2 c + 1 in
+      // sx + 1; Y_{c+1} goes into X_c's stage after HH(c), X_{c+2} into Y_c's after CY(c)
+      const int P = NC / 2;
+      dma.all(smem, 0, 0, lane);
+      ring_barrier<0>();                                   // B0: X_0 landed
+      dma.all(smem, 1, 1, lane);                           // Y_0
+      if (P > 1) dma.all(smem, 2, 2, lane);                // X_1
+      int sx = 0;
+      for (int c = 0; c < P; ++c) {
+        const bool more = c + 1 < P;
+        const int sy = sx == 2 ? 0 : sx + 1;
+        if (more) ring_barrier<G::PER>();                  // end of CX(c): Y_c landed, X_{c+1} in flight
+        else ring_barrier<0>();
+        if (more) ring_barrier<G::PER>();                  // end of HH(c): X_c's stage read
+        else ring_barrier<0>();
+        if (more) dma.all(smem, 2 * c + 3, sx, lane);      // Y_{c+1}
+        if (more) ring_barrier<G::PER>();                  // end of CY(c): X_{c+1} landed, Y_{c+1} in flight
+        else ring_barrier<0>();
+        if (c + 2 < P) dma.all(smem, 2 * c + 4, sy, lane); // X_{c+2}
+        sx = sx == 0 ? 2 : sx - 1;
+      }
+    } else if (loader) {
       dma.all(smem, 0, 0, lane);
       ring_barrier<0>();                                   // B0: chunk 0 landed
       if (NC > 1) dma.all(smem, 1, 1, lane);
@@ -2081,11 +2186,25 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       st_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
       auto mainloop = [&](auto pat_tag) {
-        int buf = 0;
-        for (int kc = 0; kc < NC; ++kc) {
-          compute(smem + buf * G::STAGE, No{}, 0, 0, Seg1{}, 0, pat_tag);
-          ring_barrier<0>();                               // B(kc+1): own LDS reads done
-          buf = buf == 2 ? 0 : buf + 1;
+        if constexpr (PX) {   // units CX(c), HH(c), CY(c) of pair c (loader schedule above)
+          int sx = 0;
+          for (int c = 0; c < NC / 2; ++c) {
+            const int sy = sx == 2 ? 0 : sx + 1;
+            compute_u(smem + sx * G::STAGE, No{}, 0, 0, Seg1{}, 0, pat_tag, UCross{}, 0);
+            ring_barrier<0>();
+            compute_u(smem + sx * G::STAGE, No{}, 0, 0, Seg1{}, 0, pat_tag, UHiHi{}, (sy - sx) * G::STAGE);
+            ring_barrier<0>();
+            compute_u(smem + sy * G::STAGE, No{}, 0, 0, Seg1{}, 0, pat_tag, UCross{}, 0);
+            ring_barrier<0>();
+            sx = sx == 0 ? 2 : sx - 1;
+          }
+        } else {
+          int buf = 0;
+          for (int kc = 0; kc < NC; ++kc) {
+            compute(smem + buf * G::STAGE, No{}, 0, 0, Seg1{}, 0, pat_tag);
+            ring_barrier<0>();                             // B(kc+1): own LDS reads done
+            buf = buf == 2 ? 0 : buf + 1;
+          }
         }
         if constexpr (G::PM && M16) {   // the last step (tap TAPS - 1) of this set's valid fragments
           constexpr int SET = decltype(pat_tag)::value;
@@ -2890,7 +3009,9 @@ static hipError_t launch_conv_xs(int kind, const ConvArgs<T>& a, hipStream_t s) 
     switch (kind) {
       case LK_UP0_F: return launch_one<T, LK_UP0_F, XS>(a, s);
       case LK_UP1_F: return launch_one<T, LK_UP1_F, XS>(a, s);
-      case LK_UP2_F: return launch_one<T, LK_UP2_F, XS>(a, s);
+      case LK_UP2_F:   // (the bf16x3 network's final level is LK_UP2_FX3)
+        if constexpr (XS == 0) return launch_one<T, LK_UP2_F, XS>(a, s);
+        break;
       case LK_UP2_FX3:
         if constexpr (XS != 0) return launch_one<T, LK_UP2_FX3, XS>(a, s);
         break;

@@ -5,8 +5,9 @@ per GPU, torch.distributed over RCCL) samples a contiguous block of the global
 (TAC, sample) index space with no per-step communication.  The noise of global
 sample g is Philox(seed, g, step), so the result is independent of the world
 size.  The only collective is one all-gather of per-(TAC, ROI, parameter)
-Welford partials {count, mean, M2} (fp64, 2,304 B per TAC), merged with Chan's
-parallel formula into the population mean / std of main_script.py:433-436.
+Welford partials {count, mean, M2} (fp64, 2,304 B per TAC) of each rank's OWN TAC
+range (padded to the largest range), merged on the host with Chan's parallel
+formula into the population mean / std of main_script.py:433-436.
 """
 from __future__ import annotations
 
@@ -24,6 +25,15 @@ def tac_major_shards(n_tac, n_per_tac, world, rank):
     """Global sample indices of `rank` for n_tac TACs x n_per_tac samples, TAC-major
     (whole TACs per rank when n_tac >= world).  Returns (lo, hi) over g = tac*n_per_tac + s."""
     return shard_range(n_tac * n_per_tac, world, rank)
+
+
+def rank_tac_range(n_tac, n_per_tac, world, rank):
+    """TACs [t0, t1) that rank `rank`'s sample block touches (t0 == t1: an empty block).  Consecutive
+    ranks' ranges overlap in at most one TAC (the TAC their blocks split)."""
+    lo, hi = tac_major_shards(n_tac, n_per_tac, world, rank)
+    if hi <= lo:
+        return lo // max(n_per_tac, 1), lo // max(n_per_tac, 1)
+    return lo // n_per_tac, (hi - 1) // n_per_tac + 1
 
 
 def merge_stats(parts):
@@ -57,7 +67,8 @@ def local_stats_numpy(x, tac=None, n_tac=1):
 
 
 def allgather_stats(stats, group=None, device=None):
-    """All-gather this rank's [n_tac_local, ...,3] partials; returns [world, ...] on the host.
+    """All-gather this rank's [n_local, ...,3] partials (every rank's array the same shape); returns
+    [world, n_local, ..., 3] on the host.
 
     Uses the process group's backend (nccl = RCCL over xGMI on MI355X, gloo on CPU)."""
     import torch
@@ -69,6 +80,26 @@ def allgather_stats(stats, group=None, device=None):
     out = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(out, t, group=group)
     return np.stack([o.cpu().numpy() for o in out])
+
+
+def gather_merge_own_tacs(local, n_tac, n_per_tac, group=None, device=None):
+    """SURVEY 8(e) payload: each rank contributes only the partials of its own TAC range (``local``:
+    [t1 - t0, 48, 2, 3] for rank_tac_range), zero-padded to the largest range over the ranks; the host
+    scatters every rank's rows to their TACs and Chan-merges (zero-count rows are neutral, and a TAC split
+    between two ranks is merged from both).  Returns the merged [n_tac, 48, 2, 3] statistics.  Each rank
+    receives world x max-range x 2,304 B (configs[3]: 8 x 32 TACs = 590 KB, not 8 x 256)."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    ranges = [rank_tac_range(n_tac, n_per_tac, world, r) for r in range(world)]
+    width = max(max(t1 - t0 for t0, t1 in ranges), 1)
+    local = np.asarray(local, dtype=np.float64)
+    pad = np.zeros((width,) + local.shape[1:])
+    pad[:local.shape[0]] = local
+    parts = allgather_stats(pad, group=group, device=device)
+    placed = np.zeros((world, n_tac) + local.shape[1:])
+    for r, (t0, t1) in enumerate(ranges):
+        placed[r, t0:t1] = parts[r, :t1 - t0]
+    return merge_stats(placed)
 
 
 def summarize(stats):
@@ -99,24 +130,26 @@ def sample_posterior_sharded(model, cond_all, n_per_tac, seed=0, x_T_seed=1, gro
     rank = dist.get_rank(group) if dist_on else 0
     n_tac = len(cond_all)
     lo, hi = tac_major_shards(n_tac, n_per_tac, world, rank)
-    stats = np.zeros((n_tac, 48, 2, 3))
+    t0, t1 = rank_tac_range(n_tac, n_per_tac, world, rank)
+    local = np.zeros((t1 - t0, 48, 2, 3))          # this rank's TACs only (the all-gather payload)
     x0 = None
     if hi > lo:
         g = np.arange(lo, hi)
         tac_g = g // n_per_tac
-        tacs = np.unique(tac_g)
+        tacs = np.arange(t0, t1)                    # contiguous: every TAC of the range has samples here
         cond = cond_all.rows(tacs) if hasattr(cond_all, 'rows') else np.asarray(cond_all)[tacs]
-        local_tac = np.searchsorted(tacs, tac_g).astype(np.int32)
+        local_tac = (tac_g - t0).astype(np.int32)
         x_T = model.philox_normal(hi - lo, seed=x_T_seed, sample_offset=lo)
         x0 = model.ddpm_loop(x_T, cond, num_timesteps=num_timesteps, seed=seed, sample_offset=lo, use_graph=use_graph,
                              tac=local_tac if len(tacs) > 1 else None)
-        st = model.posterior_stats(x0, local_tac if len(tacs) > 1 else None, n_tac=len(tacs))
-        stats[tacs] = st
+        local[:] = model.posterior_stats(x0, local_tac if len(tacs) > 1 else None, n_tac=len(tacs))
     if world > 1:
         if coll_device is None:
             coll_device = 'cpu' if dist.get_backend(group) == 'gloo' else model.device
-        parts = allgather_stats(stats, group=group, device=coll_device)
-        stats = merge_stats(parts)
+        stats = gather_merge_own_tacs(local, n_tac, n_per_tac, group=group, device=coll_device)
+    else:
+        stats = np.zeros((n_tac, 48, 2, 3))
+        stats[t0:t1] = local
     if return_samples:
         return summarize(stats), stats, (lo, hi, x0)
     return summarize(stats), stats

@@ -173,12 +173,14 @@ def _z_scale(x):
 def _rhat_basic(x):
     """Gelman-Rubin R-hat of (chains, draws, ...): sqrt((B / W + n - 1) / n) with B = n var(chain means),
     W = mean within-chain variance (ddof = 1 both).
-    W = 0 (constant chains) gives NaN without a floating-point warning; rhat() masks those parameters."""
+    W = 0 with B > 0 (chains each stuck at a different value) gives inf, as ArviZ's division does, so the
+    reference's 'rhat > 1.02' flag trips; W = B = 0 gives NaN (rhat() masks fully constant draws anyway).
+    Neither raises a floating-point warning."""
     n = x.shape[1]
     b = n * np.var(x.mean(axis=1), axis=0, ddof=1)
     w = np.mean(np.var(x, axis=1, ddof=1), axis=0)
     ok = w > 0
-    out = np.full(np.shape(w), np.nan)
+    out = np.where(b > 0, np.inf, np.nan) * np.ones(np.shape(w))
     out[ok] = np.sqrt((b[ok] / w[ok] + n - 1) / n)
     return out
 

@@ -538,8 +538,22 @@ _B128_GROUPS = [list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
 
 
 def _piece_key(row, m16):
-    """petdiff_internal.h piece_key for 64-B rows (CPR = 4)."""
-    return 2 * ((row >> 2) & 1) if m16 else (row >> 2) & 3
+    """petdiff_internal.h piece_key for 64-B rows (CPR = 4), as the library exports it (petdiff_piece_key)."""
+    from pet_posterior_distribution_amd import _lib
+    return _lib.lib().petdiff_piece_key(row, 4, int(m16))
+
+
+def test_piece_key_export_matches_documented_formula():
+    """The library's piece_key (the one kernels and host packing use) against the formulas DESIGN.md states:
+    64-B rows (row >> 2) & 3, 16x16x32 layers 2 ((row >> 2) & 1), 32-B rows (row >> 3) & 1, 128-B rows
+    (row >> 1) & 7 (the test read a Python copy of the formula before)."""
+    from pet_posterior_distribution_amd import _lib
+    L = _lib.lib()
+    for row in range(0, 2048, 3):
+        assert L.petdiff_piece_key(row, 4, 0) == (row >> 2) & 3
+        assert L.petdiff_piece_key(row, 4, 1) == 2 * ((row >> 2) & 1)
+        assert L.petdiff_piece_key(row, 2, 0) == (row >> 3) & 1 == L.petdiff_piece_key(row, 2, 1)
+        assert L.petdiff_piece_key(row, 8, 0) == (row >> 1) & 7 == L.petdiff_piece_key(row, 8, 1)
 
 
 def _b128_conflict_cycles(addr):
@@ -572,3 +586,19 @@ def test_piece_key_conflict_free_for_both_mfma_shapes(base):
     for rh in range(2):
         assert _b128_conflict_cycles(addr16(rh, True)) == 0
         assert _b128_conflict_cycles(addr16(rh, False)) > 0
+
+    # paired bf16x3 units on 16x16x32 (unet_kernels.hip PX): a cross unit reads B with its halves swapped
+    # (piece (l >> 4) ^ 2); the hi-hi unit's lanes 32-63 read piece ((l >> 4) ^ 2) of the same row in the
+    # other chunk's stage (a multiple of 256 B away: STAGE is 256-B aligned); both stay conflict-free
+    def addr16x(rh, stage_lo, stage_hi):
+        out = []
+        for l in range(64):
+            r = base + 16 * rh + (l & 15)
+            hi = l >= 32
+            out.append((stage_hi if hi else stage_lo) + r * 64 + ((((l >> 4) ^ (2 if hi or stage_lo == stage_hi
+                                                                              else 0)) ^ _piece_key(r, True)) << 4))
+        return out
+    for rh in range(2):
+        assert _b128_conflict_cycles(addr16x(rh, 0, 0)) == 0                  # cross: every lane swapped
+        assert _b128_conflict_cycles(addr16x(rh, 0, 53504)) == 0              # hi-hi: lanes 32-63 in stage Y
+        assert _b128_conflict_cycles(addr16x(rh, 107008, 0)) == 0

@@ -99,11 +99,12 @@ def test_rhat_rank_normalised_split():
 
 
 def test_rhat_constant_draws_nan_without_warnings():
-    """A parameter whose draws are constant (a chain that never moved, e.g. an un-tuned MH element) gets
-    NaN, and the within-chain variance W = 0 raises no floating-point warning (the GPU test log carried
-    divide / invalid warnings from it in round 3)."""
+    """A parameter whose draws are constant everywhere gets NaN; chains each stuck at a different value
+    (an un-tuned MH element that never accepts, W = 0 < B) get inf, as ArviZ's pm.rhat does, so the
+    reference's flag (mcmc.py:186-189) trips.  W = 0 raises no floating-point warning (the GPU test log
+    carried divide / invalid warnings from it in round 3)."""
     import warnings
-    from pet_posterior_distribution_amd.metrics import rhat
+    from pet_posterior_distribution_amd.metrics import rhat, convergence_report
     rng = np.random.default_rng(5)
     x = rng.standard_normal((4, 200, 3))
     x[..., 1] = 2.5                                      # constant everywhere
@@ -111,5 +112,13 @@ def test_rhat_constant_draws_nan_without_warnings():
     with warnings.catch_warnings():
         warnings.simplefilter('error')
         r = rhat(x)
+        rep = convergence_report(np.concatenate([x[..., :1], x[..., 2:]], axis=2), n_roi=1)
     assert np.isfinite(r[0]) and np.isnan(r[1])
-    assert np.isnan(r[2]) or r[2] > 1.02                 # W ~ 0 up to rounding: never reads as converged
+    assert r[2] > 1e6                                    # W = 0 up to the mean's rounding: inf or huge
+    assert rep['flag'] and rep['rhat_max'] > 1e6
+    from pet_posterior_distribution_amd.metrics import _rhat_basic
+    s = np.repeat(np.array([0.0, 1.0, 2.0, 3.0])[:, None, None], 10, axis=1)   # exact W = 0 < B
+    with warnings.catch_warnings():
+        warnings.simplefilter('error')
+        rb = _rhat_basic(np.concatenate([s, np.zeros_like(s)], axis=2))
+    assert rb[0] == np.inf and np.isnan(rb[1])

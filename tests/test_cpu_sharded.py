@@ -62,6 +62,25 @@ def test_tac_major_shards_split_a_tac():
     assert [tac_major_shards(N_TAC, N_PER, 2, r) for r in range(2)] == [(0, 8), (8, 15)]   # TAC 1 = g 5..9
 
 
+def test_rank_tac_ranges_and_gather_payload():
+    """Each rank gathers only its own TAC range: ranges cover every TAC, neighbours share
+    at most the TAC their blocks split, and configs[3] (256 TACs x 8192 over 8 ranks) receives 8 x 32 TACs
+    x 2,304 B per rank (<= 8 x 80 KB), not 8 x 256."""
+    from pet_posterior_distribution_amd.distributed import rank_tac_range
+    assert [rank_tac_range(N_TAC, N_PER, 2, r) for r in range(2)] == [(0, 2), (1, 3)]
+    for n_tac, n_per, world in ((3, 5, 2), (7, 3, 4), (256, 8192, 8), (2, 1, 5), (1, 1024, 1)):
+        rg = [rank_tac_range(n_tac, n_per, world, r) for r in range(world)]
+        covered = set()
+        for r, (t0, t1) in enumerate(rg):
+            lo, hi = tac_major_shards(n_tac, n_per, world, r)
+            assert set(range(t0, t1)) == set(g // n_per for g in range(lo, hi))
+            covered |= set(range(t0, t1))
+        assert covered == set(range(n_tac))
+    rg = [rank_tac_range(256, 8192, 8, r) for r in range(8)]
+    width = max(t1 - t0 for t0, t1 in rg)
+    assert width == 32 and 8 * width * 48 * 2 * 3 * 8 <= 8 * 80 * 1024
+
+
 def test_world1_matches_numpy():
     summ, st, (lo, hi, x0) = sample_posterior_sharded(StubSampler(), TacTable(N_TAC, _conds), N_PER,
                                                       return_samples=True)

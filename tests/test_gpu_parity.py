@@ -492,3 +492,34 @@ def test_p_sample_bf16_fused_levels(conds, lv, param):
     assert rel(var_t, mask * np.exp(0.5 * out['log_variance_tilde']) * z) < 1e-4
     assert float(var[-1].abs().max()) == 0.0
     m.close()
+
+
+@pytest.mark.parametrize('dtype', ['bfloat16', 'bf16x3'])
+def test_kernel_timing_reps_bitwise(conds, dtype):
+    """bench.py's per-layer timing (set_kernel_timing(reps=8): every timed launch repeated back to back
+    between its HIP events, petdiff_api.cpp launch) relies on every layer kernel being idempotent: an eager
+    loop and a p_sample timed that way are bitwise equal to the untimed ones, and each layer's launch
+    count is reps x the untimed count."""
+    rng = np.random.default_rng(31)
+    B = 150
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    t = rng.integers(0, 1000, B)
+    m = make_model(dtype)
+    m.set_kernel_timing(True, reps=1)
+    a = m.ddpm_loop(x, conds[:1], num_timesteps=12, seed=4, use_graph=False)
+    pa = m.ddpm(x, t, conds[:1], seed=6, rng_step=3)
+    torch.cuda.synchronize()
+    c1 = m.get_kernel_timing()
+    m.set_kernel_timing(True, reps=8)
+    b = m.ddpm_loop(x, conds[:1], num_timesteps=12, seed=4, use_graph=False)
+    pb = m.ddpm(x, t, conds[:1], seed=6, rng_step=3)
+    torch.cuda.synchronize()
+    c8 = m.get_kernel_timing()
+    m.set_kernel_timing(False)
+    torch.testing.assert_close(a, b, rtol=0, atol=0)
+    for u, v in zip(pa, pb):
+        torch.testing.assert_close(u, v, rtol=0, atol=0)
+    assert any(n for _, n in c1.values())
+    for name in c1:
+        assert c8[name][1] == 8 * c1[name][1], (name, c1[name], c8[name])
+    m.close()
