@@ -1570,7 +1570,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
 #define PETDIFF_URA(i, rh)                                                                                  \
   if constexpr (first(i, rh) && !(CONV_EXP_MODE & 64)) {                                                    \
     constexpr int K_ = KS * (i) + HK * (rh) + j;                                                             \
-    ucm[K_] = *reinterpret_cast<const fragT*>(ab + ((SEG == 2 ? akey2[K_] : akey1[K_]) ^ AX));               \
+    ucm[K_] = *reinterpret_cast<const fragT*>(ab + ((SEG == 2 ? akey2[K_ < UK2 ? K_ : 0] : akey1[K_]) ^ AX));  \
   }
 #define PETDIFF_URB(q, ptr) \
   if constexpr (!(CONV_EXP_MODE & 64)) bv[sb][q] = *reinterpret_cast<const fragT*>(ptr);

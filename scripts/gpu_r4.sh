@@ -9,7 +9,7 @@
 #   ldspmc   one rocprofv3 PMC pass of the LDS counters per network (bank conflicts per kernel)
 #   bench    the driver's bench command (1 GPU) and a rocprofv3 kernel-stats pass
 #   ab       REPS interleaved bench pairs: this build vs each ALT build and each ALTENVS setting (VAR=value)
-# Usage: ALTS="pre_prune.so" STAGES="bitwise tests" bash scripts/gpu_r4.sh TAG
+# Usage: ALTS="pre_prune.so" STAGES="bitwise tests" [PYTEST_K="expr"] bash scripts/gpu_r4.sh TAG
 set -o pipefail
 TAG=${1:-r4}
 STAGES=${STAGES:-"bitwise tests bench"}
@@ -30,7 +30,7 @@ if has bitwise; then
 fi
 if has tests; then
   timeout -k 10 900 python -u -m pytest tests -q -m gpu -p no:cacheprovider --timeout 200 --timeout-method thread \
-    ${PYTEST_ARGS} > $OUT/pytest.log 2>&1
+    ${PYTEST_K:+-k "$PYTEST_K"} ${PYTEST_ARGS} > $OUT/pytest.log 2>&1
   rc=$?
   echo "pytest exit $rc" >> $OUT/pytest.log
   tail -4 $OUT/pytest.log

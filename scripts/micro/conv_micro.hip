@@ -106,6 +106,14 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
   a.fin.x_all = reinterpret_cast<float*>(dbg);
 #endif
   CK(hipDeviceSynchronize());
+  if (G::EPI == EPI_FINAL) {   // launch_one's null-pointer guards (the r4f / r4g faults): refused, nothing launched
+    ConvArgs<bf16> bad = a;
+    bad.fin.x_t = nullptr;
+    const hipError_t e = launch_conv<bf16>(KIND, bad, 0, XS != 0);
+    (void)hipGetLastError();
+    if (e != hipErrorInvalidValue) { printf("null-guard FAILED: %s\n", hipGetErrorString(e)); exit(1); }
+    printf("   null-guard: a final level without x_t is refused (hipErrorInvalidValue)\n");
+  }
   for (int i = 0; i < 20; ++i) CK(launch_conv<bf16>(KIND, a, 0, XS != 0));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
