@@ -598,6 +598,16 @@ def test_piece_key_conflict_free_for_both_mfma_shapes(base):
             out.append((stage_hi if hi else stage_lo) + r * 64 + ((((l >> 4) ^ (2 if hi or stage_lo == stage_hi
                                                                               else 0)) ^ _piece_key(r, True)) << 4))
         return out
+    # the round-5 final level on 16x16x32 (measured and rejected, profiles/r05/rejected_final_level_m16.diff; 32-B
+    # rows, two taps per step): lane l reads row l & 15 (+ the tap's row shift for lanes 32-63), piece (l >> 4) & 1
+    # -- conflict-free unswizzled; the 32-row key would not be
+    def addr32b(shift, key):
+        return [((base + (l & 15) + (shift if l >= 32 else 0)) * 32 +
+                 ((((l >> 4) & 1) ^ (((base + (l & 15) + (shift if l >= 32 else 0)) >> 3) & 1 if key else 0)) << 4))
+                for l in range(64)]
+    for shift in (0, 4, 8, 96):
+        assert _b128_conflict_cycles(addr32b(shift, False)) == 0
+    assert max(_b128_conflict_cycles(addr32b(sh, True)) for sh in (0, 4, 8)) > 0
     for rh in range(2):
         assert _b128_conflict_cycles(addr16x(rh, 0, 0)) == 0                  # cross: every lane swapped
         assert _b128_conflict_cycles(addr16x(rh, 0, 53504)) == 0              # hi-hi: lanes 32-63 in stage Y
