@@ -51,7 +51,9 @@ constexpr int dma_group(int u, int pps, int kind) {
 // bit 2 the MFMAs, bit 4 the epilogue, bit 8 returns at entry, bit 16 returns after
 // the prologue DMA, bit 32 drops the ring barriers, bit 64 the
 // fragment reads (MFMAs on register operands), bit 128 stamps the main loop's
-// cycles and clock into fin.x_all.  The product is built with 0.
+// cycles and clock into fin.x_all, bit 2048 the A reads of the paired bf16x3 HH units (the upper bound of
+// reusing the cross units' A fragments for HH: -1.5 % on up0 / up1 x3, 0 on down2 / down3;
+// profiles/r05/hh_reads.txt).  The product is built with 0.
 #ifndef CONV_EXP_MODE
 #define CONV_EXP_MODE 0
 #endif
@@ -1244,7 +1246,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     mfma16_blk<3>(acc[(f) % 3][(f) / 3], zap[1][P_], bv[pb][1]);                                             \
   }
 #define PETDIFF_WRA(f)                                                                                      \
-  if constexpr (G::w6_ok(SEG, PAT, f, j) && G::w6_first(SEG, PAT, f, jj) && !(CONV_EXP_MODE & 64)) {        \
+  if constexpr (G::w6_ok(SEG, PAT, f, j) && G::w6_first(SEG, PAT, f, jj) && !(CONV_EXP_MODE & 64) && !((CONV_EXP_MODE & 2048) && UT == 2)) { \
     constexpr int P_ = G::w6_pos(SEG, PAT, f, j);                                                            \
     const int ao_ = (SEG == 2 ? apos2[P_ < G::LH ? P_ : 0] : apos1[P_]) ^ AX;                                \
     zap[0][P_] = *reinterpret_cast<const fragT*>(ab + ao_);                                                  \
@@ -1411,7 +1413,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   if constexpr (G::pw6_valid(SET, f, jp) && !(CONV_EXP_MODE & 2))                                           \
     mfma16_blk<2 * (rh) + (ch)>(acc[(f) % 3][(f) / 3], zap[rh][G::pw6_pos(SET, f) + jp - PADL], bv[pb][ch]);
 #define PETDIFF_QRA(f, rh)                                                                                  \
-  if constexpr (G::pw6_valid(SET, f, j) && G::pw6_first(SET, f, j) && !(CONV_EXP_MODE & 64)) {              \
+  if constexpr (G::pw6_valid(SET, f, j) && G::pw6_first(SET, f, j) && !(CONV_EXP_MODE & 64) && !((CONV_EXP_MODE & 2048) && UT == 2)) { \
     constexpr int P_ = G::pw6_pos(SET, f) + j - PADL;                                                        \
     zap[rh][P_] = *reinterpret_cast<const fragT*>(ab + (apm[P_] ^ AX) + (rh) * HALF);                        \
   }
@@ -1568,7 +1570,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     mfma16_blk<2 * (rh) + 1>(acc[i][1], ucm[K_], bv[pb][3]);                                                 \
   }
 #define PETDIFF_URA(i, rh)                                                                                  \
-  if constexpr (first(i, rh) && !(CONV_EXP_MODE & 64)) {                                                    \
+  if constexpr (first(i, rh) && !(CONV_EXP_MODE & 64) && !((CONV_EXP_MODE & 2048) && UT == 2)) {            \
     constexpr int K_ = KS * (i) + HK * (rh) + j;                                                             \
     ucm[K_] = *reinterpret_cast<const fragT*>(ab + ((SEG == 2 ? akey2[K_ < UK2 ? K_ : 0] : akey1[K_]) ^ AX));  \
   }
@@ -2501,6 +2503,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
 #endif
 #if CONV_EXP_MODE & 128
     if (tid == 0) reinterpret_cast<unsigned long long*>(a.fin.x_all)[4096 + 2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the end stamp after the workgroup's stores drained
     __syncthreads();
     if (tid == 0) reinterpret_cast<unsigned long long*>(a.fin.x_all)[8192 + 4 * blockIdx.x + 3] =
         __builtin_amdgcn_s_memrealtime();
