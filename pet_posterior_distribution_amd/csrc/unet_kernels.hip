@@ -431,7 +431,16 @@ struct ConvGeom {
   }
   // first tile row of wave wm's fragment i
   static __device__ __forceinline__ int frag_row(int wm, int i) { return wm * 96 + i * 32; }
-  static constexpr int CT_LD = 2 * NT + 8;          // fp32 C tile, one ROW PAIR [c][2] per line (non-final)
+  // the row-pair epilogue of the generic (not position-major, not fused) 64-column layers: down1, and the unfused
+  // up convs of the fp32 / unfused networks.  Its C-tile and map reads take row pairs rp .. rp + 3 per
+  // ds_read_b128 lane group, 8 lanes a row ("down1's epilogue conflicts").
+  static constexpr bool GEN64 = !PM && !W6 && !FUSED && EPI != EPI_FINAL && NT == 64;
+  // fp32 C tile, one ROW PAIR [c][2] per line (non-final).  GEN64: a line of 132 floats (4 banks past a
+  // multiple of 64) puts the four row pairs of a lane group on disjoint banks (136: 2-way conflicts)
+  static constexpr int CT_LD = 2 * NT + (GEN64 ? 4 : 8);
+  // GEN64: 16-B piece c of map row l sits in LDS slot c ^ map_swz(l), so the lane group's row pairs at
+  // equal column (rows 2 rp and 2 rp + 6 apart) read different banks (unswizzled rows are 64 floats: 2-way)
+  static __device__ __host__ constexpr int map_swz(int l) { return GEN64 ? (l >> 1) & 1 : 0; }
   static constexpr int FIN_LD = 132;                // fp32 C tile row (final epilogue, 16-B aligned)
   // FINAL: C tile | final kernel [128][4] | x_next rows [MT][2] (fused next-step down0)
   // the non-final C tile is staged in EPI_PARTS row blocks (co-residency experiment: 2, half the LDS)
@@ -1933,7 +1942,9 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         } else {
           if (!on) continue;
           if (q < G::MAP_PIECES) {
-            const int l = q / (NT / 4), c = q - l * (NT / 4);
+            const int l = q / (NT / 4);
+            int c = q - l * (NT / 4);
+            if constexpr (G::GEN64) c ^= G::map_swz(l);   // slot q <- piece (l, c)
             const int row = is_c ? tac0 : a.t_uniform;
             const int off = (((row * L + l) * a.cout) + n_tile * NT + c * 4) * 4;
             llvm_amdgcn_raw_buffer_load_lds(is_c ? rs_c : rs_t,
@@ -2416,7 +2427,13 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
           const f32x4 c0v = {cq[0][e], cq[0][2 + e], cq[1][e], cq[1][2 + e]};
           const f32x4 c1v = {cq[2][e], cq[2][2 + e], cq[3][e], cq[3][2 + e]};
           f32x4 m0v = ep_b0, m1v = ep_b1;
-          if constexpr (MODE == 1) {
+          if constexpr (MODE == 1 && G::GEN64) {
+            const int sw = 4 * G::map_swz(le);   // pieces nloc / 4 and nloc / 4 + 1 (nloc is a multiple of 8)
+            m0v = *reinterpret_cast<const f32x4*>(lt + le * NT + (nloc + sw)) +
+                  *reinterpret_cast<const f32x4*>(lc + le * NT + (nloc + sw));
+            m1v = *reinterpret_cast<const f32x4*>(lt + le * NT + (nloc + 4 - sw)) +
+                  *reinterpret_cast<const f32x4*>(lc + le * NT + (nloc + 4 - sw));
+          } else if constexpr (MODE == 1) {
             m0v = *reinterpret_cast<const f32x4*>(lt + le * NT + nloc) +
                   *reinterpret_cast<const f32x4*>(lc + le * NT + nloc);
             m1v = *reinterpret_cast<const f32x4*>(lt + le * NT + nloc + 4) +
