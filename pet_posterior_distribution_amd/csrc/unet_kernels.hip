@@ -51,7 +51,8 @@ constexpr int dma_group(int u, int pps, int kind) {
 // bit 2 the MFMAs, bit 4 the epilogue, bit 8 returns at entry, bit 16 returns after
 // the prologue DMA, bit 32 drops the ring barriers, bit 64 the
 // fragment reads (MFMAs on register operands), bit 128 stamps the main loop's
-// cycles and clock into fin.x_all, bit 2048 the A reads of the paired bf16x3 HH units (the upper bound of
+// cycles and clock into fin.x_all, bit 4096 stages half of chunk 0 in the prologue (wrong outputs; the maps
+// and condition indices the epilogue indexes with stay loaded), bit 2048 the A reads of the paired bf16x3 HH units (the upper bound of
 // reusing the cross units' A fragments for HH: -1.5 % on up0 / up1 x3, 0 on down2 / down3;
 // profiles/r05/hh_reads.txt).  The product is built with 0.
 #ifndef CONV_EXP_MODE
@@ -701,6 +702,13 @@ struct DmaPlan {
   }
 
   __device__ __forceinline__ void all(char* smem, int kc, int buf, int lane) const {
+    if constexpr ((CONV_EXP_MODE & 4096) != 0) {   // diagnostic: chunk 0 (the prologue) stages half its pieces
+      if (kc == 0) {
+#pragma unroll
+        for (int k = 0; k < G::PER / 2; ++k) piece(smem + buf * G::STAGE, k, kc, lane);
+        return;
+      }
+    }
     if (G::FUSED && kc >= n1) {
 #pragma unroll
       for (int k = 0; k < G::PER2; ++k) piece(smem + buf * G::STAGE, k, kc, lane);
