@@ -612,3 +612,32 @@ def test_piece_key_conflict_free_for_both_mfma_shapes(base):
         assert _b128_conflict_cycles(addr16x(rh, 0, 0)) == 0                  # cross: every lane swapped
         assert _b128_conflict_cycles(addr16x(rh, 0, 53504)) == 0              # hi-hi: lanes 32-63 in stage Y
         assert _b128_conflict_cycles(addr16x(rh, 107008, 0)) == 0
+
+
+def test_down1_epilogue_reads_conflict_free():
+    """down1's row-pair epilogue (unet_kernels.hip GEN64: 64 output columns, 8 lanes a row pair, L = 24):
+    thread t reads row pair rp = t / 8 + 32 i (6 passes) at columns 8 (t % 8) .. + 7, i.e. four 16-B pieces
+    of its C-tile line and two 16-B pieces of each of the time / label map rows l, l + 1 (l = 2 rp mod 24).
+    With 136-float lines and unswizzled 64-float map rows this costs 1,152 extra LDS cycles per workgroup:
+    294,912 per launch over 256 workgroups, the epilogue's share of the PMC count (profiles/r05/r5i:
+    442,624 -> 147,712).  The round-5 layout (132-float lines, map piece c of row l in slot c ^ ((l >> 1) & 1))
+    is conflict-free."""
+    def extra(ct_ld, swz):
+        total = 0
+        for w in range(4):
+            for it in range(6):
+                rp = [(64 * w + l) // 8 + 32 * it for l in range(64)]
+                c = [(64 * w + l) % 8 for l in range(64)]
+                for k in range(4):
+                    total += _b128_conflict_cycles([4 * (rp[l] * ct_ld + 16 * c[l] + 4 * k) for l in range(64)])
+                for e in range(2):
+                    for half in range(2):
+                        addr = []
+                        for l in range(64):
+                            le = (2 * rp[l]) % 24 + e
+                            g = (le >> 1) & 1 if swz else 0
+                            addr.append(4 * (le * 64 + 4 * ((2 * c[l] + half) ^ g)))
+                        total += 2 * _b128_conflict_cycles(addr)        # the time and the label map
+        return total
+    assert extra(136, False) == 1152
+    assert extra(132, True) == 0
