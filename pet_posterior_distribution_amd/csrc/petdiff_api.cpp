@@ -138,6 +138,15 @@ struct petdiff_ctx {
   bool fuse_up = false;
   DevBuf wpack_f[3], epack_f[3];     // packed composite weights / left-edge correction weights
   DevBuf tmap_f[3], cmap_f[3];       // u-path maps through the block conv (+ block biases)
+  // One condition (n_tac == 1): the time and label maps summed once per schedule / condition change,
+  // cmb = tmap[t] + cmap[0] in fp32 (the sum every epilogue formed before adding the accumulators, so
+  // the outputs are bitwise the same), passed as the non-final layers' tmap with cmap null: their
+  // epilogues stage and read one map instead of two.  down0 and the final level keep both tables (the
+  // final level's transposed epilogue measured slower on one).
+  // PETDIFF_COMBINE_MAPS=0 keeps the two tables everywhere (A/B switch).
+  bool combine_ok = true;
+  bool use_cmb = false;
+  DevBuf cmb[7], cmb_f[3];
   DevBuf tab;                        // [kNTab][T]
   DevBuf temb, tseq;                 // [T][48], scratch [T][L]
   int T = 0;
@@ -368,6 +377,35 @@ int fused_maps(petdiff_ctx* h, int u, bool time, int n, hipStream_t s) {
   return PETDIFF_OK;
 }
 
+// the combined tables of a one-condition handle (see petdiff_ctx::cmb); called whenever the schedule or the
+// conditions change.  A reallocated table invalidates the captured graphs (they hold its address).
+int combine_maps(petdiff_ctx* h, hipStream_t s) {
+  h->use_cmb = false;
+  if (!h->combine_ok || !h->sched_set || h->n_tac != 1) return PETDIFF_OK;
+  bool moved = false;
+  auto one = [&](DevBuf& dst, const DevBuf& tm, const DevBuf& cm, size_t per) -> hipError_t {
+    const void* old = dst.p;
+    hipError_t e = dst.alloc((size_t)h->T * per * 4);
+    if (e != hipSuccess) return e;
+    moved = moved || (old != nullptr && old != dst.p);
+    return launch_add_rows(tm.as<float>(), cm.as<float>(), per, (size_t)h->T * per, dst.as<float>(), s);
+  };
+  // the non-final layers' tables (down0 and the final level keep the two tables)
+  for (int lv = 1; lv < 7; ++lv)
+    HIPC(one(h->cmb[lv], h->tmap[lv], h->cmap[lv], (size_t)kLevels[lv].Lout * kLevels[lv].cout));
+  if (h->fuse_up)
+    for (int u = 0; u < 2; ++u) HIPC(one(h->cmb_f[u], h->tmap_f[u], h->cmap_f[u], (size_t)kFused[u].L * kFused[u].cout));
+  if (moved) {
+    for (auto& kv : h->graphs) {
+      if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+      if (kv.second.graph) (void)hipGraphDestroy(kv.second.graph);
+    }
+    h->graphs.clear();
+  }
+  h->use_cmb = true;
+  return PETDIFF_OK;
+}
+
 int ensure_workspace(petdiff_ctx* h, int B) {
   if (B > PETDIFF_MAX_BATCH) return fail(PETDIFF_ERR_INVALID, "batch exceeds PETDIFF_MAX_BATCH (65536); split it into chunks");
   if (B <= h->B_cap) return PETDIFF_OK;
@@ -500,8 +538,10 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
       a.wpack = h->wpack_f[u].as<T>();
       a.epack = h->epack_f[u].as<T>();
       a.out = reinterpret_cast<T*>(lio[li].out);
-      a.tmap = h->tmap_f[u].as<float>();
-      a.cmap = h->cmap_f[u].as<float>();
+      // the final level keeps both tables (its transposed epilogue and fused down0 measured slower on one)
+      const bool cmb = h->use_cmb && li != kNumConvLayers - 1;
+      a.tmap = (cmb ? h->cmb_f[u] : h->tmap_f[u]).as<float>();
+      a.cmap = cmb ? nullptr : h->cmap_f[u].as<float>();
       a.tac = io.tac;
       a.tvec = io.tvec;
       a.t_uniform = io.t_uniform;
@@ -533,8 +573,9 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
     a.out = reinterpret_cast<T*>(lio[li].out);
     a.out_pool = reinterpret_cast<T*>(lio[li].pool);
     if (cl.cond_level >= 0) {
-      a.cmap = h->cmap[cl.cond_level].as<float>();
-      a.tmap = h->tmap[cl.cond_level].as<float>();
+      const bool cmb = h->use_cmb && li != kNumConvLayers - 1;
+      a.cmap = cmb ? nullptr : h->cmap[cl.cond_level].as<float>();
+      a.tmap = (cmb ? h->cmb[cl.cond_level] : h->tmap[cl.cond_level]).as<float>();
     } else {
       a.bias = h->bias_only[li].as<float>();
     }
@@ -671,6 +712,7 @@ int petdiff_create(const petdiff_config* cfg, const float* weights, size_t n_wei
   HIPC(hipSetDevice(device));
   HIPC(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
   if (const char* e = std::getenv("PETDIFF_GRAPH_SEG")) h->seg_steps = std::max(0, std::atoi(e));
+  if (const char* e = std::getenv("PETDIFF_COMBINE_MAPS")) h->combine_ok = std::atoi(e) != 0;
   HIPC(h->w32.alloc(need * 4));
   HIPC(hipMemcpy(h->w32.p, weights, need * 4, hipMemcpyHostToDevice));
   std::vector<float> host(weights, weights + need);
@@ -761,6 +803,8 @@ int petdiff_set_schedule(petdiff_handle h, const float* tables, int T) {
     for (int u = 0; u < 3; ++u) CHK(fused_maps(h, u, true, T, 0));
   HIPC(hipDeviceSynchronize());
   h->sched_set = true;
+  CHK(combine_maps(h, 0));
+  HIPC(hipDeviceSynchronize());
   return PETDIFF_OK;
 }
 
@@ -799,6 +843,7 @@ int petdiff_set_conditions(petdiff_handle h, const float* cond, int n_tac, void*
     h->graphs.clear();
   }
   h->n_tac = n_tac;
+  CHK(combine_maps(h, s));
   return PETDIFF_OK;
 }
 

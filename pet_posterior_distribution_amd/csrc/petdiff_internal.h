@@ -111,6 +111,8 @@ hipError_t launch_compose(const float* wup, int cin_up, int xoff, int cbn, int c
 hipError_t launch_map_through(const float* in, int n, int L, int cu, const float* kblk, const float* kres, int taps,
                               int padl, int cin_blk, int ch0, const float* b1, const float* b2, float* out, int cout,
                               hipStream_t s);
+// out[i] = a[i] + b[i % per] (fp32), i < n: the combined time + label map table of a one-condition handle
+hipError_t launch_add_rows(const float* a, const float* b, size_t per, size_t n, float* out, hipStream_t s);
 hipError_t launch_philox_normal(unsigned long long seed, unsigned long long goff, int step, int B, float* out,
                                 hipStream_t s);
 hipError_t launch_posterior_stats(const float* x0, const int* tac, int B, int n_tac, int ncol,

@@ -523,3 +523,43 @@ def test_kernel_timing_reps_bitwise(conds, dtype):
     for name in c1:
         assert c8[name][1] == 8 * c1[name][1], (name, c1[name], c8[name])
     m.close()
+
+
+@pytest.mark.parametrize('dtype', ['bfloat16', 'float16', 'float32', 'bf16x3'])
+def test_combined_maps_bitwise(conds, dtype, monkeypatch):
+    """One condition: the epilogues read one combined time + label table (tmap[t] + cmap[0], formed once per
+    schedule / condition change, petdiff_api.cpp combine_maps) instead of two.  The sum is the one every
+    epilogue formed before adding its accumulators, so the outputs are bit-identical to the two-table path
+    (PETDIFF_COMBINE_MAPS=0): forward with one t and with per-sample t (the epilogue's general path),
+    p_sample, the graph and eager loops, and after the handle moves to two conditions and back."""
+    rng = np.random.default_rng(31)
+    B = 45
+    x = rng.standard_normal((B, 48, 2)).astype(np.float32)
+    t_vec = rng.integers(0, 1000, B).astype(np.int32)
+    monkeypatch.setenv('PETDIFF_COMBINE_MAPS', '0')
+    two = make_model(dtype)
+    two._ensure_handle()                       # the switch is read when the handle is created
+    monkeypatch.setenv('PETDIFF_COMBINE_MAPS', '1')
+    one = make_model(dtype)
+    one._ensure_handle()
+
+    def same(fa, fb):
+        ra, rb = fa(two), fb(one)
+        for u, v in zip(ra if isinstance(ra, tuple) else (ra,), rb if isinstance(rb, tuple) else (rb,)):
+            torch.testing.assert_close(u, v, rtol=0, atol=0)
+    c1 = conds[:1]
+    for t in (np.full(B, 617, np.int32), t_vec):
+        f = lambda m: m.call({'x': x, 'time': t, 'condition': c1})  # noqa: E731
+        same(f, f)
+    f = lambda m: m.ddpm(x, np.full(B, 311, np.int32), condition=c1, seed=3)  # noqa: E731
+    same(f, f)
+    for g in (True, False):
+        f = lambda m: m.ddpm_loop(x, c1, num_timesteps=20, seed=6, use_graph=g)  # noqa: E731
+        same(f, f)
+    tac = rng.integers(0, 2, B).astype(np.int32)                # two conditions: both handles use two tables
+    f = lambda m: m.ddpm_loop(x, conds[:2], num_timesteps=12, seed=2, tac=tac)  # noqa: E731
+    same(f, f)
+    f = lambda m: m.ddpm_loop(x, conds[1:2], num_timesteps=12, seed=2)  # noqa: E731  back to one condition
+    same(f, f)
+    two.close()
+    one.close()
