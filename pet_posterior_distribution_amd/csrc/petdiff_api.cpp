@@ -391,7 +391,8 @@ int combine_maps(petdiff_ctx* h, hipStream_t s) {
     return launch_add_rows(tm.as<float>(), cm.as<float>(), per, (size_t)h->T * per, dst.as<float>(), s);
   };
   // the non-final layers' tables (down0 and the final level keep the two tables)
-  for (int lv = 1; lv < 7; ++lv)
+  // (the fused path's up levels read cmb_f; their k2-conv levels 4-6 then run no layer)
+  for (int lv = 1; lv < (h->fuse_up ? 4 : 7); ++lv)
     HIPC(one(h->cmb[lv], h->tmap[lv], h->cmap[lv], (size_t)kLevels[lv].Lout * kLevels[lv].cout));
   if (h->fuse_up)
     for (int u = 0; u < 2; ++u) HIPC(one(h->cmb_f[u], h->tmap_f[u], h->cmap_f[u], (size_t)kFused[u].L * kFused[u].cout));
