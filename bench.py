@@ -680,34 +680,57 @@ def mh_config2_and_protocol(iddpm_10k_s, dev, cpu=True):
 
 def weights_sensitivity(net, cond, B, dev, reps=3):
     """The step's speed depends on the weight VALUES: the chip holds its clock by power under this load, and
-    MFMA energy depends on operand bit activity.  Same workload as `value` with all-zero weights (the power
-    floor: MFMA operands toggle nothing) and, when scripts/train_protocol.py's output is present, with the
-    trained network (weights/trained_r02.npz).  Context for `value`, which uses random-init weights."""
+    MFMA energy depends on operand bit activity.  The same workload as `value` (configs[1]: B samples x 1000
+    steps, one generate() per rep) for bf16 and bf16x3 with:
+      * glorot: the headline's own random-init weights (UnetConditional(seed=1234)), re-timed here beside the
+        others so the ratios are same-process;
+      * trained: the shipped network after 800 Adam steps on GPU-simulated training data
+        (tests/helpers.quick_trained_weights: batch 256, lr 2e-4, clipnorm 1.5 as main_script.py:169-174,
+        regenerated in-process, about 3 s), an eps-predictor whose reverse chain stays bounded;
+      * zeros: all-zero weights (the power floor: MFMA operands toggle nothing);
+      * trained_r02: scripts/train_protocol.py's longer-trained network, when weights/trained_r02.npz exists.
+    Context for `value`, which uses the glorot weights."""
     import torch
     from pet_posterior_distribution_amd import ImprovedDDPM
     from pet_posterior_distribution_amd.configs import shipped_diff_args
     keep = net.weights
-    variants = {'zeros': {k: np.zeros_like(v) for k, v in keep.items()}}
+    variants = {'glorot': keep}
+    try:
+        from tests.helpers import quick_trained_weights
+        variants['trained'] = quick_trained_weights()[0]
+    except Exception as e:   # noqa: BLE001 -- reported, not fatal: the headline line must still print
+        variants['trained_error'] = repr(e)
+    variants['zeros'] = {k: np.zeros_like(v) for k, v in keep.items()}
     tw = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'weights', 'trained_r02.npz')
     if os.path.exists(tw):
         with np.load(tw) as z:
             variants['trained_r02'] = {k: z[k] for k in keep}
-    out = {}
+    out = {'reps': reps, 'n_posterior': B, 'reverse_steps': 1000}
     try:
-        for name, w in variants.items():
-            net.weights = w
-            m = ImprovedDDPM(network=net, dtype='bfloat16', device=dev.index, **shipped_diff_args())
-            x = m.philox_normal(B, seed=1)
-            m.ddpm_loop(x, cond[None], seed=2)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(reps):
+        for dtype, tag in (('bfloat16', ''), ('bf16x3', 'bf16x3_')):
+            for name, w in variants.items():
+                if isinstance(w, str):
+                    out[name] = w
+                    continue
+                net.weights = w
+                m = ImprovedDDPM(network=net, dtype=dtype, device=dev.index, **shipped_diff_args())
+                x = m.philox_normal(B, seed=1)
                 m.ddpm_loop(x, cond[None], seed=2)
-            torch.cuda.synchronize()
-            out[name + '_samples_per_s'] = round(reps * B / (time.perf_counter() - t0), 1)
-            m.close()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    y = m.ddpm_loop(x, cond[None], seed=2)
+                torch.cuda.synchronize()
+                out[tag + name + '_samples_per_s'] = round(reps * B / (time.perf_counter() - t0), 1)
+                if name == 'trained':
+                    out[tag + 'trained_outputs_finite'] = bool(torch.isfinite(y).all())
+                m.close()
     finally:
         net.weights = keep
+    for tag in ('', 'bf16x3_'):
+        g, t = out.get(tag + 'glorot_samples_per_s'), out.get(tag + 'trained_samples_per_s')
+        if g and t:
+            out[tag + 'trained_over_glorot'] = round(t / g, 4)
     return out
 
 
@@ -796,14 +819,19 @@ def main():
         elapsed = max_over_ranks(elapsed, dev)
     _, allst, (lo, hi, out) = res
     assert (lo, hi) == (offset, offset + B)
-    if world > 1:                              # the all-gather alone, timed once after the loop
-        from pet_posterior_distribution_amd.distributed import gather_merge_own_tacs, rank_tac_range
+    if world > 1:                              # the all-gather alone, and the host merge, timed once after the loop
+        from pet_posterior_distribution_amd.distributed import (allgather_stats, merge_gathered_tacs,
+                                                                pad_own_tacs, rank_tac_range)
         t0r, t1r = rank_tac_range(len(allst), n_per, world, rank)
+        pad = pad_own_tacs(allst[t0r:t1r], len(allst), n_per, world)
         torch.cuda.synchronize()
         ta = time.perf_counter()
-        gather_merge_own_tacs(allst[t0r:t1r], len(allst), n_per, device=coll)
+        parts = allgather_stats(pad, device=coll)      # the collective on the padded own-TAC partials only
         torch.cuda.synchronize()
         ag['ms'] = (time.perf_counter() - ta) * 1e3
+        tb = time.perf_counter()
+        merge_gathered_tacs(parts, len(allst), n_per)
+        ag['merge_ms'] = (time.perf_counter() - tb) * 1e3
     ag_ms = ag['ms']
     finite = bool(torch.isfinite(out).all())
     x_T = model.philox_normal(min(B, chunk), seed=1, sample_offset=offset)
@@ -841,6 +869,8 @@ def main():
             'roofline': roof,
             'outputs_finite': finite,
             'stats_allgather_ms': round(ag_ms, 3),
+            # host placement + Chan merge of the gathered rows (gather_merge_own_tacs minus its all-gather)
+            'stats_merge_ms': round(ag.get('merge_ms', 0.0), 3),
             # bytes each rank receives: world x the largest rank's TAC range x 2,304 B (own TACs only)
             'stats_allgather_bytes': world * max(t1 - t0 for t0, t1 in (rank_tac_range(world * n_tac, n_per, world, r)
                                                                         for r in range(world))) * 48 * 2 * 3 * 8,

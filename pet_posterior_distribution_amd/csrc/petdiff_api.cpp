@@ -377,32 +377,43 @@ int fused_maps(petdiff_ctx* h, int u, bool time, int n, hipStream_t s) {
   return PETDIFF_OK;
 }
 
+// destroy every captured graph (they hold the addresses of the tables and the workspace)
+void clear_graphs(petdiff_ctx* h) {
+  for (auto& kv : h->graphs) {
+    if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+    if (kv.second.graph) (void)hipGraphDestroy(kv.second.graph);
+  }
+  h->graphs.clear();
+}
+
 // the combined tables of a one-condition handle (see petdiff_ctx::cmb); called whenever the schedule or the
 // conditions change.  A reallocated table invalidates the captured graphs (they hold its address).
 int combine_maps(petdiff_ctx* h, hipStream_t s) {
   h->use_cmb = false;
   if (!h->combine_ok || !h->sched_set || h->n_tac != 1) return PETDIFF_OK;
-  bool moved = false;
-  auto one = [&](DevBuf& dst, const DevBuf& tm, const DevBuf& cm, size_t per) -> hipError_t {
-    const void* old = dst.p;
-    hipError_t e = dst.alloc((size_t)h->T * per * 4);
+  const int nlv = h->fuse_up ? 4 : 7;
+  auto need = [&](int lv) { return (size_t)h->T * kLevels[lv].Lout * kLevels[lv].cout * 4; };
+  auto need_f = [&](int u) { return (size_t)h->T * kFused[u].L * kFused[u].cout * 4; };
+  // a table that has to grow is freed and reallocated, so the graphs that hold its address go first (also
+  // when an allocation or launch below fails: no graph survives that could replay a freed table)
+  bool grow = false;
+  for (int lv = 1; lv < nlv; ++lv) grow = grow || h->cmb[lv].bytes < need(lv) || !h->cmb[lv].p;
+  if (h->fuse_up)
+    for (int u = 0; u < 2; ++u) grow = grow || h->cmb_f[u].bytes < need_f(u) || !h->cmb_f[u].p;
+  if (grow) clear_graphs(h);
+  auto one = [&](DevBuf& dst, const DevBuf& tm, const DevBuf& cm, size_t bytes) -> hipError_t {
+    hipError_t e = dst.alloc(bytes);
     if (e != hipSuccess) return e;
-    moved = moved || (old != nullptr && old != dst.p);
-    return launch_add_rows(tm.as<float>(), cm.as<float>(), per, (size_t)h->T * per, dst.as<float>(), s);
+    return launch_add_rows(tm.as<float>(), cm.as<float>(), bytes / 4 / h->T, bytes / 4, dst.as<float>(), s);
   };
   // the non-final layers' tables (down0 and the final level keep the two tables)
   // (the fused path's up levels read cmb_f; their k2-conv levels 4-6 then run no layer)
-  for (int lv = 1; lv < (h->fuse_up ? 4 : 7); ++lv)
-    HIPC(one(h->cmb[lv], h->tmap[lv], h->cmap[lv], (size_t)kLevels[lv].Lout * kLevels[lv].cout));
+  hipError_t e = hipSuccess;
+  for (int lv = 1; lv < nlv && e == hipSuccess; ++lv) e = one(h->cmb[lv], h->tmap[lv], h->cmap[lv], need(lv));
   if (h->fuse_up)
-    for (int u = 0; u < 2; ++u) HIPC(one(h->cmb_f[u], h->tmap_f[u], h->cmap_f[u], (size_t)kFused[u].L * kFused[u].cout));
-  if (moved) {
-    for (auto& kv : h->graphs) {
-      if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
-      if (kv.second.graph) (void)hipGraphDestroy(kv.second.graph);
-    }
-    h->graphs.clear();
-  }
+    for (int u = 0; u < 2 && e == hipSuccess; ++u) e = one(h->cmb_f[u], h->tmap_f[u], h->cmap_f[u], need_f(u));
+  if (e != hipSuccess) clear_graphs(h);   // the tables are partly rewritten: no captured graph may replay them
+  HIPC(e);
   h->use_cmb = true;
   return PETDIFF_OK;
 }
@@ -431,11 +442,7 @@ int ensure_workspace(petdiff_ctx* h, int B) {
   HIPC(h->tbuf.alloc(Bz * 4));
   HIPC(h->rng.alloc(16));
   // workspace moved: cached graphs hold stale pointers
-  for (auto& kv : h->graphs) {
-    if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
-    if (kv.second.graph) (void)hipGraphDestroy(kv.second.graph);
-  }
-  h->graphs.clear();
+  clear_graphs(h);
   h->B_cap = B;
   h->last_B = 0;   // the level buffers are new: nothing to read back until a forward / p_sample runs
   return PETDIFF_OK;
@@ -780,6 +787,9 @@ int petdiff_destroy(petdiff_handle h) {
 int petdiff_set_schedule(petdiff_handle h, const float* tables, int T) {
   CHK(valid_handle(h));
   if (!tables || T <= 0) return fail(PETDIFF_ERR_INVALID, "bad schedule tables");
+  // tab, tmap and tmap_f may be reallocated and are rewritten: no captured graph may keep replaying them
+  clear_graphs(h);
+  h->use_cmb = false;
   HIPC(h->tab.alloc((size_t)kNTab * T * 4));
   HIPC(hipMemcpy(h->tab.p, tables, (size_t)kNTab * T * 4, hipMemcpyHostToDevice));
   h->T = T;
@@ -814,6 +824,12 @@ int petdiff_set_conditions(petdiff_handle h, const float* cond, int n_tac, void*
   if (!cond || n_tac <= 0) return fail(PETDIFF_ERR_INVALID, "bad conditions");
   hipStream_t s = (hipStream_t)stream;
   const int rows = n_tac * h->cfg.n_cond_rows;
+  // a new TAC count reallocates cmap / cmap_f (and changes which map tables the layers read): the
+  // captured graphs go before any table moves
+  if (n_tac != h->n_tac) {
+    clear_graphs(h);
+    h->use_cmb = false;
+  }
   HIPC(h->enc_a.alloc((size_t)rows * 256 * 4));
   HIPC(h->enc_b.alloc((size_t)rows * 256 * 4));
   float* A = h->enc_a.as<float>();
@@ -836,13 +852,6 @@ int petdiff_set_conditions(petdiff_handle h, const float* cond, int n_tac, void*
   }
   if (h->fuse_up)
     for (int u = 0; u < 3; ++u) CHK(fused_maps(h, u, false, n_tac, s));
-  if (n_tac != h->n_tac) {
-    for (auto& kv : h->graphs) {
-      if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
-      if (kv.second.graph) (void)hipGraphDestroy(kv.second.graph);
-    }
-    h->graphs.clear();
-  }
   h->n_tac = n_tac;
   CHK(combine_maps(h, s));
   return PETDIFF_OK;
@@ -953,7 +962,8 @@ int petdiff_generate(petdiff_handle h, const float* x_T, const int32_t* tac, con
     std::vector<hipGraphExec_t> ex((size_t)nseg);
     for (int sg = 0; sg < nseg; ++sg) {
       const int i0 = sg * seg, i1 = std::min(n_steps, i0 + seg);
-      std::vector<int> key{B, flag_var_tilde, tac ? 1 : 0, n_steps, i0, i1};
+      // (use_cmb and T: the captured layers read the combined or the two map tables of this schedule)
+      std::vector<int> key{B, flag_var_tilde, tac ? 1 : 0, n_steps, i0, i1, h->use_cmb ? 1 : 0, h->T};
       key.insert(key.end(), t_seq, t_seq + n_steps);
       auto it = h->graphs.find(key);
       if (it == h->graphs.end()) {

@@ -3026,6 +3026,11 @@ static hipError_t launch_one(const ConvArgs<T>& a, hipStream_t s) {
   if (a.B <= 0) return hipSuccess;
   if (a.cout % G::NT != 0 || a.c1 % G::KC != 0 || a.c2 % G::KC != 0) return hipErrorInvalidValue;
   if (G::FUSED && (!a.src2 || !a.epack || a.c2 <= 0)) return hipErrorInvalidValue;
+  // paired bf16x3 units on a fused 16x16x32 level (conv_body's PX schedule): pair 0, the segment-1 -> 2
+  // transition pair and segment 2's first pair are peeled, so each segment needs >= 2 pairs of 16-channel
+  // chunks (P1 = c1 / KC, P - P1 = c2 / KC); up0 / up1 have 16 / 8 and 32 / 16
+  if constexpr (XS != 0 && G::FUSED && G::M16G && DmaPlan<T, KIND, XS>::P3)
+    if (a.c1 / G::KC < 2 || a.c2 / G::KC < 2) return hipErrorInvalidValue;
   // the fused final level's transposed epilogue reads the packed final kernel and both map tables
   if (G::FIN_MAPS && (!a.fin.wf4 || !a.tmap || !a.cmap)) return hipErrorInvalidValue;
   if (G::EPI == EPI_FINAL) {   // every pointer the final epilogue dereferences unconditionally

@@ -90,14 +90,25 @@ def gather_merge_own_tacs(local, n_tac, n_per_tac, group=None, device=None):
     receives world x max-range x 2,304 B (configs[3]: 8 x 32 TACs = 590 KB, not 8 x 256)."""
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    ranges = [rank_tac_range(n_tac, n_per_tac, world, r) for r in range(world)]
-    width = max(max(t1 - t0 for t0, t1 in ranges), 1)
+    return merge_gathered_tacs(allgather_stats(pad_own_tacs(local, n_tac, n_per_tac, world), group=group,
+                                               device=device), n_tac, n_per_tac)
+
+
+def pad_own_tacs(local, n_tac, n_per_tac, world):
+    """This rank's [t1 - t0, ...] partials zero-padded to the widest rank range (the all-gather payload)."""
+    width = max(max(t1 - t0 for t0, t1 in (rank_tac_range(n_tac, n_per_tac, world, r) for r in range(world))), 1)
     local = np.asarray(local, dtype=np.float64)
     pad = np.zeros((width,) + local.shape[1:])
     pad[:local.shape[0]] = local
-    parts = allgather_stats(pad, group=group, device=device)
-    placed = np.zeros((world, n_tac) + local.shape[1:])
-    for r, (t0, t1) in enumerate(ranges):
+    return pad
+
+
+def merge_gathered_tacs(parts, n_tac, n_per_tac):
+    """[world, width, ...] gathered payloads -> every rank's rows placed at their TACs, Chan-merged."""
+    world = parts.shape[0]
+    placed = np.zeros((world, n_tac) + parts.shape[2:])
+    for r in range(world):
+        t0, t1 = rank_tac_range(n_tac, n_per_tac, world, r)
         placed[r, t0:t1] = parts[r, :t1 - t0]
     return merge_stats(placed)
 

@@ -75,6 +75,22 @@ if has ldspmc; then
     grep -E "^(down|up)" $OUT/lds_$d.txt
   done
 fi
+if has mhpmc; then
+  # configs[2]'s chain kernel (10k chains, mh_chain_kernel) on a short run: its time unprofiled, then one
+  # rocprofv3 PMC pass per counter group (instruction mix, issue / wait cycles, LDS, fetched bytes)
+  MHAPP="python $GRAFT_REPO_ROOT/bench.py --workload mh --mh-iters 300 --mh-tune 300 --no-cpu-baseline"
+  timeout -k 10 120 $MHAPP > $OUT/mh_short.json 2> $OUT/mh_short.err || { echo "mh short failed"; exit 1; }
+  timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/mhpmc/kt -o run --output-format csv -- $MHAPP > $OUT/mhpmc_kt.log 2>&1 || { echo "mh kt failed"; exit 1; }
+  i=0
+  for CTR in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
+             "SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_SMEM SQ_INSTS_BRANCH" \
+             "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT SQ_INST_CYCLES_SALU" \
+             "FETCH_SIZE" "WRITE_SIZE"; do
+    i=$((i+1))
+    timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $CTR -d $GRAFT_REPO_ROOT/$OUT/mhpmc/p$i -o run --output-format csv -- $MHAPP > $OUT/mhpmc_p$i.log 2>&1 || { echo "mh pmc pass $i failed"; tail -5 $OUT/mhpmc_p$i.log; exit 1; }
+  done
+  head -c 300 $OUT/mh_short.json; echo
+fi
 if has bench; then
   timeout -k 10 500 python bench.py --gpus 1 --steps 20 --warmup 5 ${BENCH_EXTRA} > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail $OUT/bench.err; exit 1; }
   head -c 400 $OUT/bench.json; echo

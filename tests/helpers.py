@@ -27,6 +27,29 @@ def mh_problem(g2, case=0, noise=0.1, seed=0):
                 Cov_DVR=pr['Cov_DVR'], mu_R1=truth_R * 0.98, Cov_R1=pr['Cov_R1'])
 
 
+def assert_same_distribution(x, y, z_mean=5.0, z_cov=5.5, ks_alpha=1e-3):
+    """x (n, d) and y (m, d) independent draws of one distribution: every marginal mean within z_mean
+    Monte-Carlo standard errors, every covariance entry within z_cov standard errors of the difference
+    (se of a sample covariance entry from the fourth moments: var((x_i - m_i)(x_j - m_j)) / n), and every
+    marginal passes a two-sample Kolmogorov-Smirnov test at ks_alpha after a Bonferroni split over d.
+    Returns the largest statistics (for the test's message)."""
+    import numpy as np
+    from scipy.stats import ks_2samp
+    x, y = np.asarray(x, np.float64), np.asarray(y, np.float64)
+    n, m, d = len(x), len(y), x.shape[1]
+    se = np.sqrt(x.var(0, ddof=1) / n + y.var(0, ddof=1) / m)
+    zm = np.abs(x.mean(0) - y.mean(0)) / se
+    cx, cy = x - x.mean(0), y - y.mean(0)
+    px, py = cx[:, :, None] * cx[:, None, :], cy[:, :, None] * cy[:, None, :]
+    zc = np.abs(px.mean(0) - py.mean(0)) / np.sqrt(px.var(0, ddof=1) / n + py.var(0, ddof=1) / m)
+    pks = np.array([ks_2samp(x[:, k], y[:, k]).pvalue for k in range(d)])
+    stats = dict(z_mean=float(zm.max()), z_cov=float(zc.max()), ks_p_min=float(pks.min()))
+    assert zm.max() < z_mean, stats
+    assert zc.max() < z_cov, stats
+    assert pks.min() > ks_alpha / d, stats
+    return stats
+
+
 _TRAINED = {}
 
 

@@ -88,3 +88,17 @@ def test_generator_statistics_and_sharding():
     # sample g's draw does not depend on how the set is split
     part = simulate_dataset(16, seed=3, sample_offset=100, sigma_noise=d['sigma_noise'])
     torch.testing.assert_close(part['tac_noisy_sampled'], d['tac_noisy_sampled'][100:116], rtol=0, atol=0)
+
+
+def test_generator_prior_vs_reference_sampler_draws():
+    """varDVR / varR1 of the GPU generator against draws of the reference's own sampler (G8:
+    helper_func.truncnormal_samples + the SRTM2 redraw loop of sample_sim_data.py:139-188, generated by
+    tests/golden/make_prior_golden.py): means, covariances and per-marginal KS (tests/helpers)."""
+    import os
+    from tests.helpers import assert_same_distribution
+    from pet_posterior_distribution_amd.sim_data import simulate_dataset
+    with np.load(os.path.join(os.path.dirname(__file__), 'golden', 'g8_prior_draws.npz')) as z:
+        g8 = {k: z[k] for k in z.files}
+    d = simulate_dataset(4096, seed=21)
+    print(assert_same_distribution(d['varDVR'].cpu().numpy(), g8['dvr_sel']),
+          assert_same_distribution(d['varR1'].cpu().numpy(), g8['r1_sel']))
