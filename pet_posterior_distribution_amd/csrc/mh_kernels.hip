@@ -51,6 +51,17 @@ __device__ __forceinline__ double log_phi_poly(const double* tab, double x) {
   return p;
 }
 
+// 1/sqrt(x) for a positive normal x: v_rsq_f64, then two Newton steps y (1 + (1/2 - x y^2 / 2)) in fma form
+__device__ __forceinline__ double rsq_f64(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const double r = fma(-(x * y), 0.5 * y, 0.5);
+    y = fma(y, r, y);
+  }
+  return y;
+}
+
 // e^{-k2a t} of the update kernel by fp64_math.h exp_fast (<= 1 ulp) instead of ocml's exp
 #ifndef MH_FAST_EXP
 #define MH_FAST_EXP 0
@@ -58,6 +69,19 @@ __device__ __forceinline__ double log_phi_poly(const double* tab, double x) {
 // log of the noise scale sigma > 0 (MH_FAST_LOG): fp64_math.h log_pos
 #ifndef MH_FAST_LOG
 #define MH_FAST_LOG 1
+#endif
+// Round 6: the per-frame noise terms from r = 1/sqrt(sn) (v_rsq_f64 + two Newton steps) and a table of 1/SIG
+// (exact, formed at LDS load): 1/sig = r / SIG, z = (y - sn) / sig, xs = sn / sig, log sig = -log(1/sig).
+// It replaces ocml's correctly rounded sqrt and the IEEE division 1 / sig (about 20 fp64 instructions a
+// frame) by 8; the terms move by an ulp or two, so accept / reject paths can differ from the oracles' only
+// where log u lies within ~1e-15 of the ratio.  0: sqrt and divide (the oracles' expression order)
+#ifndef MH_RSQ
+#define MH_RSQ 0
+#endif
+// Round 6: the sweep's per-element LDS operands (the next element's index, proposal draw, log u and prior
+// diagonal) read one element ahead, so their LDS round trips overlap the current element's likelihood
+#ifndef MH_PF
+#define MH_PF 0
 #endif
 
 // LDS copy of the coefficient table (one element per thread)
@@ -172,6 +196,9 @@ __device__ __forceinline__ double roi_loglik(const Lds& s, const double2 (&mreg)
     const double conv = c0 + c1;
     const double tac = r1 * s.CR[lane] + (k2 - r1 * k2a) * conv;   // :157-158
     const double sn = tac < 0.0 ? 1e-6 : tac;                       // mcmc.py:152
+#if MH_RSQ
+    const double inv = rsq_f64(sn) * s.SIG[i * NF + lane];         // SIG holds 1/SIG (load_lds)
+#else
 #if MH_EXP_MODE & 8
     const double sig = sn * s.SIG[i * NF + lane];
 #else
@@ -182,6 +209,7 @@ __device__ __forceinline__ double roi_loglik(const Lds& s, const double2 (&mreg)
 #else
     const double inv = 1.0 / sig;
 #endif
+#endif
     const double z = (s.Y[i * NF + lane] - sn) * inv;
     const double xs = sn * inv;
     // log Phi(x) for x >= 10 is -7.6e-24 or smaller: 0 at the precision of the sum
@@ -190,7 +218,9 @@ __device__ __forceinline__ double roi_loglik(const Lds& s, const double2 (&mreg)
 #else
     const double lnd = xs < 10.0 ? (MH_LOGPHI_POLY ? log_phi_poly(s.LPHI, xs) : log_ndtr(xs)) : 0.0;
 #endif
-#if MH_EXP_MODE & 2
+#if MH_RSQ
+    l = -0.5 * z * z - 0.9189385332046727 + log_pos(inv) - lnd;      // - log sig = log(1 / sig)
+#elif MH_EXP_MODE & 2
     l = -0.5 * z * z - 0.9189385332046727 - sig - lnd;
 #else
     l = -0.5 * z * z - 0.9189385332046727 - (MH_FAST_LOG ? log_pos(sig) : log(sig)) - lnd;
@@ -206,7 +236,7 @@ __device__ void load_lds(Lds& s, const MHConst& c) {
     s.M[k] = g < NF ? c.M[g * NF + f] : 0.0;   // global operator is [g][f]
   }
   for (int k = threadIdx.x; k < NR * NR; k += blockDim.x) { s.PD[k] = c.PD[k]; s.PR[k] = c.PR[k]; }
-  for (int k = threadIdx.x; k < NR * NF; k += blockDim.x) { s.Y[k] = c.Y[k]; s.SIG[k] = c.SIG[k]; }
+  for (int k = threadIdx.x; k < NR * NF; k += blockDim.x) { s.Y[k] = c.Y[k]; s.SIG[k] = MH_RSQ ? 1.0 / c.SIG[k] : c.SIG[k]; }
   for (int k = threadIdx.x; k < NF; k += blockDim.x) { s.CR[k] = c.CR[k]; s.TV[k] = c.TV[k]; }
   for (int k = threadIdx.x; k < NR; k += blockDim.x) { s.MUD[k] = c.MUD[k]; s.MUR[k] = c.MUR[k]; }
   load_logphi(s.LPHI);
@@ -317,23 +347,56 @@ __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun 
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       double run = 0.0;                  // log p(running) - log p(sweep start)
+#if MH_PF
+      // element j's (k, Z_k, log u_k) were read during element j - 1, element j + 1's order index during j - 1
+      int k_cur = __builtin_amdgcn_readfirstlane(ORDw[0]);
+      int k_nxt = __builtin_amdgcn_readfirstlane(ORDw[1]);
+      double z_cur = Zw[k_cur], lu_cur = LUw[k_cur];
+#endif
 #pragma unroll 1
       for (int j = 0; j < 2 * NR; ++j) {
+#if MH_PF
+        const int k = k_cur;
+        const int ord2 = ORDw[j + 2 < 2 * NR ? j + 2 : 2 * NR - 1];
+        const double z_nxt = Zw[k_nxt], lu_nxt = LUw[k_nxt];
+        const double zk = z_cur, luk = lu_cur;
+#else
         const int k = __builtin_amdgcn_readfirstlane(ORDw[j]);
+#endif
         const int v = k >= NR, i = v ? k - NR : k;
         const double* P = v ? s.PR : s.PD;
+#if MH_PF
+        const double pii = P[i * NR + i], pli = P[li * NR + i];
+#endif
         const double Di = lane_bcast(D, i), Ri = lane_bcast(R, i);
         const double xi = v ? Ri : Di;
         const double si = v ? lane_bcast(sR, i) : lane_bcast(sD, i);
         const double gi = v ? lane_bcast(gR, i) : lane_bcast(gD, i);
         const double lli = lane_bcast(ll, i);
+#if MH_PF
+        const double delta = zk * si;
+#else
         const double delta = Zw[k] * si;
+#endif
         const double xp = xi + delta;
-        const double dprior = -0.5 * (2.0 * delta * gi + delta * delta * P[i * NR + i]);
         const double lln = roi_loglik(s, mreg, e, lane, i, v ? Di : xp, v ? xp : Ri, c.k2p);
+#if MH_PF
+        const double dprior = -0.5 * (2.0 * delta * gi + delta * delta * pii);
+#else
+        const double dprior = -0.5 * (2.0 * delta * gi + delta * delta * P[i * NR + i]);
+#endif
         const double step = dprior + lln - lli;
         const double mr = r.vs_sweep_start ? run + step : step;
-        if (isfinite(mr) && LUw[k] < mr) {   // wave-uniform decision (metrop_select)
+#if MH_PF
+        const bool acc_ = isfinite(mr) && luk < mr;
+        k_cur = k_nxt;
+        z_cur = z_nxt;
+        lu_cur = lu_nxt;
+        k_nxt = __builtin_amdgcn_readfirstlane(ord2);
+#else
+        const bool acc_ = isfinite(mr) && LUw[k] < mr;
+#endif
+        if (acc_) {   // wave-uniform decision (metrop_select)
           run += step;
           if (lane == i) {
             if (v == 0) { D = xp; aD += 1; if (it >= r.n_tune) accD += 1.0; }
@@ -341,8 +404,13 @@ __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun 
             ll = lln;
           }
           if (own) {
+#if MH_PF
+            if (v == 0) gD = fma(delta, pli, gD);
+            else gR = fma(delta, pli, gR);
+#else
             if (v == 0) gD = fma(delta, P[lane * NR + i], gD);
             else gR = fma(delta, P[lane * NR + i], gR);
+#endif
           }
         }
       }
@@ -509,15 +577,23 @@ __device__ __forceinline__ void eval_batch(const LdsB& s, double* W, double* P, 
       const double z = (s.Y[i * NF + lane] - sn) * sig;
       l = -0.5 * z * z - 0.9189385332046727 - sig;
 #else
+#if MH_RSQ
+      const double inv = rsq_f64(sn) * s.SIG[i * NF + lane];             // SIG holds 1/SIG
+#else
       const double sig = sqrt(sn) * s.SIG[i * NF + lane];                 // :153
       const double inv = 1.0 / sig;
+#endif
       const double z = (s.Y[i * NF + lane] - sn) * inv;
       const double xs = sn * inv;
       // log Phi(xs) (log_ndtr): xs = sqrt(sn) / SIG >= 0 or NaN, so only its x > -1 branch
       // log(erfc(-x / sqrt 2) / 2) is reachable (NaN falls through to NaN either way)
       const double lnd = xs < 10.0 ? (MH_LOGPHI_POLY ? log_phi_poly(s.LPHI, xs)
                                                       : log(0.5 * erfc(-xs * 0.7071067811865476))) : 0.0;
+#if MH_RSQ
+      l = -0.5 * z * z - 0.9189385332046727 + log_pos(inv) - lnd;
+#else
       l = -0.5 * z * z - 0.9189385332046727 - (MH_FAST_LOG ? log_pos(sig) : log(sig)) - lnd;
+#endif
 #endif
     }
     W[q * 64 + lane] = l;
@@ -546,7 +622,7 @@ __global__ __launch_bounds__(kBW * 64) void mh_chain_batched(MHConst c, MHRun r)
     const int f = k / MLD, g = k - f * MLD;
     s.M[k] = g < NF ? c.M[g * NF + f] : 0.0;   // global operator is [g][f]
   }
-  for (int k = threadIdx.x; k < NR * NF; k += blockDim.x) { s.Y[k] = c.Y[k]; s.SIG[k] = c.SIG[k]; }
+  for (int k = threadIdx.x; k < NR * NF; k += blockDim.x) { s.Y[k] = c.Y[k]; s.SIG[k] = MH_RSQ ? 1.0 / c.SIG[k] : c.SIG[k]; }
   for (int k = threadIdx.x; k < NR * NR; k += blockDim.x) { s.PD[k] = c.PD[k]; s.PR[k] = c.PR[k]; }
   for (int k = threadIdx.x; k < NF; k += blockDim.x) { s.CR[k] = c.CR[k]; s.TV[k] = c.TV[k]; }
   for (int k = threadIdx.x; k < NR; k += blockDim.x) { s.MUD[k] = c.MUD[k]; s.MUR[k] = c.MUR[k]; }

@@ -141,8 +141,9 @@ struct petdiff_ctx {
   // One condition (n_tac == 1): the time and label maps summed once per schedule / condition change,
   // cmb = tmap[t] + cmap[0] in fp32 (the sum every epilogue formed before adding the accumulators, so
   // the outputs are bitwise the same), passed as the non-final layers' tmap with cmap null: their
-  // epilogues stage and read one map instead of two.  down0 and the final level keep both tables (the
-  // final level's transposed epilogue measured slower on one).
+  // epilogues stage and read one map instead of two.  The fused final level reads it too (round 6: its
+  // transposed epilogue stages the tile's rows in LDS, CONV_FIN_REGMAPS); down0 and the unfused final level
+  // keep both tables.
   // PETDIFF_COMBINE_MAPS=0 keeps the two tables everywhere (A/B switch).
   bool combine_ok = true;
   bool use_cmb = false;
@@ -399,19 +400,19 @@ int combine_maps(petdiff_ctx* h, hipStream_t s) {
   bool grow = false;
   for (int lv = 1; lv < nlv; ++lv) grow = grow || h->cmb[lv].bytes < need(lv) || !h->cmb[lv].p;
   if (h->fuse_up)
-    for (int u = 0; u < 2; ++u) grow = grow || h->cmb_f[u].bytes < need_f(u) || !h->cmb_f[u].p;
+    for (int u = 0; u < 3; ++u) grow = grow || h->cmb_f[u].bytes < need_f(u) || !h->cmb_f[u].p;
   if (grow) clear_graphs(h);
   auto one = [&](DevBuf& dst, const DevBuf& tm, const DevBuf& cm, size_t bytes) -> hipError_t {
     hipError_t e = dst.alloc(bytes);
     if (e != hipSuccess) return e;
     return launch_add_rows(tm.as<float>(), cm.as<float>(), bytes / 4 / h->T, bytes / 4, dst.as<float>(), s);
   };
-  // the non-final layers' tables (down0 and the final level keep the two tables)
+  // the non-final layers' tables and the fused final level's (down0 and the unfused final level keep two)
   // (the fused path's up levels read cmb_f; their k2-conv levels 4-6 then run no layer)
   hipError_t e = hipSuccess;
   for (int lv = 1; lv < nlv && e == hipSuccess; ++lv) e = one(h->cmb[lv], h->tmap[lv], h->cmap[lv], need(lv));
   if (h->fuse_up)
-    for (int u = 0; u < 2 && e == hipSuccess; ++u) e = one(h->cmb_f[u], h->tmap_f[u], h->cmap_f[u], need_f(u));
+    for (int u = 0; u < 3 && e == hipSuccess; ++u) e = one(h->cmb_f[u], h->tmap_f[u], h->cmap_f[u], need_f(u));
   if (e != hipSuccess) clear_graphs(h);   // the tables are partly rewritten: no captured graph may replay them
   HIPC(e);
   h->use_cmb = true;
@@ -546,8 +547,9 @@ int run_network(petdiff_ctx* h, const StepIO& io, int B, hipStream_t s) {
       a.wpack = h->wpack_f[u].as<T>();
       a.epack = h->epack_f[u].as<T>();
       a.out = reinterpret_cast<T*>(lio[li].out);
-      // the final level keeps both tables (its transposed epilogue and fused down0 measured slower on one)
-      const bool cmb = h->use_cmb && li != kNumConvLayers - 1;
+      // (the final level reads the combined table too: its transposed epilogue stages the tile's rows in LDS
+      // during the K loop, CONV_FIN_REGMAPS; its fused next-step down0 keeps level 0's two tables)
+      const bool cmb = h->use_cmb;
       a.tmap = (cmb ? h->cmb_f[u] : h->tmap_f[u]).as<float>();
       a.cmap = cmb ? nullptr : h->cmap_f[u].as<float>();
       a.tac = io.tac;

@@ -46,6 +46,18 @@ constexpr int dma_group(int u, int pps, int kind) {
 #ifndef CONV_FIN_LDS_MAPS
 #define CONV_FIN_LDS_MAPS 0
 #endif
+// Round 6: the fused final level's map rows (t uniform, one condition per tile) and its final kernel wf4 loaded
+// to registers by all 256 threads (6 + 6 coalesced 16-B loads, one wf4 piece) before the K loop's
+// second-to-last chunk, and written to LDS after the loop; the transposed epilogue reads them from LDS
+// instead of 48 map and 32 wf4 loads per lane from L2 (0: the round-5 epilogue)
+#ifndef CONV_FIN_REGMAPS
+#define CONV_FIN_REGMAPS 1
+#endif
+static_assert(!(CONV_FIN_REGMAPS && CONV_FIN_LDS_MAPS), "one final-level map path");
+// where the 3-stage final level issues those loads: 2 = before chunk NC - 2, 1 = before the last chunk
+#ifndef CONV_FIN_REGMAPS_AT
+#define CONV_FIN_REGMAPS_AT 2
+#endif
 
 // Diagnostic builds only (scripts/micro/conv_micro.hip): bit 1 drops the K-loop DMA,
 // bit 2 the MFMAs, bit 4 the epilogue, bit 8 returns at entry, bit 16 returns after
@@ -479,6 +491,15 @@ struct ConvGeom {
   static constexpr int FMAP_BYTES = FIN_LDS ? (FMAP_FULL * kThreads + (FMAP_REM + 63) / 64 * 64) * 16 : 0;
   static constexpr int SMEM1 = SMEM0 > TAIL ? SMEM0 : TAIL;
   static constexpr int SMEM = FIN_MAPS ? FMAP_OFF + FMAP_BYTES : SMEM1;
+  // fused final level (CONV_FIN_REGMAPS): the tile's map rows tmap[t] + cmap[tac] as [L][FIN_LD] fp32 and the
+  // final kernel wf4 [128][4], loaded to registers by every thread during the K loop's second-to-last chunk and
+  // written to LDS after the loop, past the transposed epilogue's partials / down0 maps (24 KB) and x_next rows
+  static constexpr int FRM_PIECES = L * (NT / 4);               // 16-B pieces of one map (6 per thread)
+  static constexpr int FRM_PT = FRM_PIECES / kThreads;
+  static constexpr int FRM_OFF = 26 * 1024;
+  static constexpr int FRW_OFF = FRM_OFF + L * FIN_LD * 4;
+  static_assert(!FIN_MAPS || (FRM_PIECES % kThreads == 0 && FRW_OFF + 128 * 16 <= SMEM &&
+                              FRM_OFF >= 48 * 128 * 4 + MT * 2 * 4 + 64), "final-level map rows in LDS");
   static_assert(!FIN_MAPS || (TAIL == 0 && FIN_LD == 132 && NT == 128), "final map layout");
   static_assert(!PREMAP || EPI_BYTES <= MAP_OFF, "C tile must not overlap the prefetched maps");
   // Dedicated loader waves (16-bit 3-stage layers): 4 extra waves issue every LDS-DMA
@@ -2001,6 +2022,26 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       if (wv * 64 < G::FMAP_REM) piece(G::FMAP_FULL);
     }
   };
+  // CONV_FIN_REGMAPS: the final level's map rows (t uniform, the handle's combined table: cmap null) and wf4 as
+  // register loads issued in the K loop's last chunks (behind every LDS-DMA; the ring wait that retires them
+  // comes one chunk later), written to LDS after the loop; the transposed epilogue then reads both from LDS
+  bool fin_reg = false;
+  f32x4 frm[G::FIN_MAPS ? G::FRM_PT : 1], frw = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (TF && CONV_FIN_REGMAPS)   // one combined table tmap[t] + cmap[0] (a one-condition handle)
+    fin_reg = a.t_uniform >= 0 && a.tmap && !a.cmap;
+  auto fin_reg_issue = [&]() {
+    if constexpr (TF && CONV_FIN_REGMAPS) {
+      if (fin_reg) {
+        const float* mt = a.tmap + (size_t)a.t_uniform * L * a.cout;
+#pragma unroll
+        for (int k = 0; k < G::FRM_PT; ++k) {
+          const int q = tid + kThreads * k, l = q / (NT / 4), c = q - l * (NT / 4);
+          frm[k] = *reinterpret_cast<const f32x4*>(mt + l * a.cout + 4 * c);
+        }
+      }
+      if (tid < 128) frw = *reinterpret_cast<const f32x4*>(a.fin.wf4 + 4 * tid);
+    }
+  };
   // LDS-DMA instructions per wave issued by the two prefetches (fused levels): NMAPW, or NMAPW + 1
   // for the waves that issue the final maps' partial instruction
   constexpr int NMAPW = (G::PREMAP && G::FUSED ? G::NPI_MAP : 0) + (G::FIN_LDS ? G::FMAP_FULL : 0);
@@ -2031,6 +2072,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         wait_vmcnt<0>();
         __syncthreads();
       }
+      fin_reg_issue();   // (lands during the last chunk)
       compute(smem + (kc & 1) * G::STAGE, No{}, 0, 0, Seg2{}, kc, P0{});
       __syncthreads();
     } else {
@@ -2109,9 +2151,12 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
           ring_barrier<G::PER2>();
           buf = buf == 2 ? 0 : buf + 1;
         }
+        // (behind chunk NC - 1's DMA: both land during chunk NC - 2, the ring wait after it retires them)
+        if constexpr (CONV_FIN_REGMAPS_AT == 2) fin_reg_issue();
         compute(smem + buf * G::STAGE, No{}, 0, 0, Seg2{}, kc, pat_tag);
         ring_barrier<0>();
         buf = buf == 2 ? 0 : buf + 1;
+        if constexpr (CONV_FIN_REGMAPS_AT == 1) fin_reg_issue();   // (lands during the last chunk)
         compute(smem + buf * G::STAGE, No{}, 0, 0, Seg2{}, kc + 1, pat_tag);
         ring_barrier<0>();
        }
@@ -2568,6 +2613,66 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     const bool fuse_next = f.next.t_uniform >= 0 && f.x_next != nullptr;
     if constexpr (TF) {
       static_assert(!TF || (G::WM == 2 && G::WN == 2 && G::FUSED && G::PHROWS == 96), "TF: one phase per wave row");
+#if CONV_FIN_REGMAPS
+      // the combined map rows tmap[t] + cmap[0] (combine_maps: the fp32 sum the two-table add forms) and wf4,
+      // loaded during the K loop
+      float* frl = reinterpret_cast<float*>(smem + G::FRM_OFF);
+      if (fin_reg) {
+#pragma unroll
+        for (int k = 0; k < G::FRM_PT; ++k) {
+          const int q = tid + kThreads * k, l = q / (NT / 4), c = q - l * (NT / 4);
+          *reinterpret_cast<f32x4*>(frl + l * G::FIN_LD + 4 * c) = frm[k];
+        }
+      }
+      if (tid < 128) *reinterpret_cast<f32x4*>(smem + G::FRW_OFF + 16 * tid) = frw;
+      __syncthreads();
+      const float* wfs = reinterpret_cast<const float*>(smem + G::FRW_OFF);
+      // per row: o4 accumulates over (jn, g, q) in the same order as the register-wq loop below (bitwise equal)
+      f32x4 o3[3] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      const float* mrow[3][2];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int r = wm * 96 + 32 * i + lr;
+        int sr, lr_;
+        G::row_sl(r, sr, lr_);
+        const int br = min(m0 + sr, B - 1);
+        if (fin_reg) {
+          mrow[i][0] = frl + lr_ * G::FIN_LD;
+          mrow[i][1] = nullptr;
+        } else {
+          const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[br];
+          const int tac = a.tac ? a.tac[br] : 0;
+          mrow[i][0] = a.tmap + ((size_t)t * L + lr_) * cout;
+          mrow[i][1] = a.cmap ? a.cmap + ((size_t)tac * L + lr_) * cout : nullptr;   // (null: combined table)
+        }
+      }
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int n = wn * 64 + jn * 32 + 8 * g + 4 * h;
+          f32x4 wq4[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) wq4[q] = *reinterpret_cast<const f32x4*>(wfs + (n + q) * 4);
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            const f32x4 hv = (fin_reg || !mrow[i][1]) ? *reinterpret_cast<const f32x4*>(mrow[i][0] + n)
+                                                      : *reinterpret_cast<const f32x4*>(mrow[i][0] + n) +
+                                                            *reinterpret_cast<const f32x4*>(mrow[i][1] + n);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float hq = fmaxf(acc[i][jn][4 * g + q] + hv[q], 0.f);
+              o3[i][0] = fmaf(hq, wq4[q][0], o3[i][0]);
+              o3[i][1] = fmaf(hq, wq4[q][1], o3[i][1]);
+              o3[i][2] = fmaf(hq, wq4[q][2], o3[i][2]);
+              o3[i][3] = fmaf(hq, wq4[q][3], o3[i][3]);
+            }
+          }
+        }
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        *reinterpret_cast<f32x4*>(fin + ((wn * 2 + h) * G::MT + wm * 96 + 32 * i + lr) * 4) = o3[i];
+#else
       f32x4 wq[2][4][4];                              // wf4 rows of this lane's 32 channels
 #pragma unroll
       for (int jn = 0; jn < 2; ++jn)
@@ -2611,6 +2716,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
           }
         *reinterpret_cast<f32x4*>(fin + ((wn * 2 + h) * G::MT + r) * 4) = o4;
       }
+#endif
     } else {
 #pragma unroll
       for (int i = 0; i < 3; ++i)
@@ -3032,7 +3138,8 @@ static hipError_t launch_one(const ConvArgs<T>& a, hipStream_t s) {
   if constexpr (XS != 0 && G::FUSED && G::M16G && DmaPlan<T, KIND, XS>::P3)
     if (a.c1 / G::KC < 2 || a.c2 / G::KC < 2) return hipErrorInvalidValue;
   // the fused final level's transposed epilogue reads the packed final kernel and both map tables
-  if (G::FIN_MAPS && (!a.fin.wf4 || !a.tmap || !a.cmap)) return hipErrorInvalidValue;
+  // (CONV_FIN_REGMAPS: cmap null = tmap is the handle's combined table tmap[t] + cmap[0])
+  if (G::FIN_MAPS && (!a.fin.wf4 || !a.tmap || (!a.cmap && !CONV_FIN_REGMAPS))) return hipErrorInvalidValue;
   if (G::EPI == EPI_FINAL) {   // every pointer the final epilogue dereferences unconditionally
     const FinalArgs& f = a.fin;
     if (!f.wf || !f.bf || f.n_out < 1 || f.n_out > 4) return hipErrorInvalidValue;

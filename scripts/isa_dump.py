@@ -93,7 +93,41 @@ def compare(pa, pb):
     return 1 if bad else 0
 
 
+def regs(path=None, pattern='conv_kernel'):
+    """Per-kernel register / LDS / scratch figures from the code object's AMDGPU metadata note."""
+    from pet_posterior_distribution_amd import _lib
+    co = code_object(path or _lib.LIB_PATH)
+    with tempfile.NamedTemporaryFile(suffix='.elf') as f:
+        f.write(co)
+        f.flush()
+        txt = subprocess.run([OBJDUMP.replace('objdump', 'readelf'), '--notes', f.name], check=True,
+                             capture_output=True, text=True).stdout
+    rows, cur = [], {}
+    for line in txt.splitlines():
+        m = re.match(r'\s*-?\s*\.(\w+):\s+(\S+)', line)
+        if not m:
+            continue
+        k, v = m.groups()
+        if k == 'agpr_count' and cur:     # a kernel's map starts with .agpr_count in this metadata layout
+            rows.append(cur)
+            cur = {}
+        cur[k] = v
+    rows.append(cur)
+    out = []
+    for r in rows:
+        if pattern in r.get('name', ''):
+            out.append((r['name'], int(r.get('vgpr_count', -1)), int(r.get('agpr_count', -1)),
+                        int(r.get('sgpr_count', -1)), int(r.get('group_segment_fixed_size', -1)),
+                        int(r.get('private_segment_fixed_size', -1)), int(r.get('vgpr_spill_count', -1))))
+    for o in out:
+        print(f'{o[0]:60s} vgpr {o[1]:4d} agpr {o[2]:4d} sgpr {o[3]:3d} lds {o[4]:6d} scratch {o[5]:4d} spill {o[6]}')
+    return out
+
+
 if __name__ == '__main__':
+    if sys.argv[1] == 'regs':
+        regs(sys.argv[2] if len(sys.argv) > 2 else None)
+        sys.exit(0)
     if sys.argv[1] == 'dump':
         dump(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
     else:

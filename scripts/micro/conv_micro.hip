@@ -78,6 +78,9 @@ void run(const char* name, int B, int c1, int c2, int cout, int iters) {
   a.src1 = s1; a.c1 = c1; a.src2 = s2; a.c2 = c2; a.wpack = w; a.out = out; a.out_pool = pool;
   a.cmap = cmap; a.tmap = tmap; a.bias = bias; a.tac = nullptr; a.tvec = nullptr; a.t_uniform = 500;
   a.B = B; a.cout = cout; a.n_t = 1000; a.n_tac = 1;
+  // the fused final level of a one-condition handle reads one combined map table (CONV_FIN_REGMAPS, as the
+  // product: petdiff_api.cpp passes cmb_f[2] and no label map)
+  if (G::FIN_MAPS && CONV_FIN_REGMAPS) a.cmap = nullptr;
   // wf: [128][4] (n_out = 4), which is also the packed wf4 layout the fused final level reads
   a.fin.wf = wf; a.fin.wf4 = wf; a.fin.bf = bfv; a.fin.n_out = 4; a.fin.x_t = xt; a.fin.z = nullptr; a.fin.rng = rng;
   a.fin.rng_step = 3; a.fin.tab = tab; a.fin.T = 1000; a.fin.learn_mode = 2; a.fin.param_mode = 0;
@@ -291,6 +294,10 @@ int main(int argc, char** argv) {
   const char* only = argc > 2 ? argv[2] : "";
   if (std::string(only) == "u2") {   // the final level alone
     run<LK_UP2_F>("up2.fused", B, 128, 256, 128, it);
+    return 0;
+  }
+  if (std::string(only) == "u2x") {   // the bf16x3 final level alone
+    run<LK_UP2_FX3, 1>("up2.fused.x3", B, 128, 256, 128, it);
     return 0;
   }
   if (std::string(only) == "d1") {   // down1 alone (co-residency experiment: B = 1024 and 2048)
