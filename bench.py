@@ -382,6 +382,41 @@ def layer_us(layer_ms):
 MH_FP64_FLOP_PER_UPDATE = 2 * 54 * 54 + 54 * 120
 
 
+def mh_roofline(chain_steps_per_s, launch_chain_steps):
+    """configs[2]'s chain kernel against the bound it hits (round 6).  The kernel is
+    issue-bound, not fp64-FLOP-bound: its waves spend ~55 % of their cycles issuing, ~34 % waiting on LDS /
+    wave barriers (PMC, SQ_ACTIVE_INST_ANY / SQ_WAIT_ANY / SQ_WAVE_CYCLES).  The committed PMC summary
+    (profiles/mh_pmc.json, scripts/mh_pmc_summary.py, stamped with the MH code object's hash) gives the
+    instruction mix per element update; the VALU pipe's cycles per update are fp64 wave64 instructions x 4 +
+    the other VALU x 2 (MI355X_MICROARCH.md).  achieved = live updates/s x those cycles, peak = 1024 SIMDs x
+    2.4 GHz; traffic = the counted fabric bytes of one 10k-chain launch scaled to this launch's chain-steps.
+    The fp64 FLOP figure of earlier rounds stays as fp64_tflops / fp64_frac (an estimate, 12,312 FLOP per
+    update).  Counters of another build: every counter-derived field None, pmc_stale True."""
+    from pet_posterior_distribution_amd import _lib
+    fl = chain_steps_per_s * 96 * MH_FP64_FLOP_PER_UPDATE / 1e12
+    out = {'bound': 'valu-issue', 'achieved': None, 'peak': round(1024 * 2.4, 1), 'unit': 'G VALU-pipe cycles/s',
+           'frac': None, 'traffic': None, 'fp64_tflops': round(fl, 2), 'fp64_frac': round(fl / 78.6, 4),
+           'flop_per_update': MH_FP64_FLOP_PER_UPDATE}
+    try:
+        with open(os.path.join(ROOT, 'profiles', 'mh_pmc.json')) as f:
+            d = json.load(f)
+    except Exception:
+        d = {}
+    now = _lib.kernel_code_hash(b'mh_chain_kernel')
+    out['pmc_stale'] = not d or d.get('code_hash') != now
+    if not out['pmc_stale']:
+        cyc = d['valu_pipe_cycles_per_update']
+        ach = chain_steps_per_s * 96 * cyc / 1e9
+        out.update({'achieved': round(ach, 1), 'frac': round(ach / out['peak'], 4),
+                    'traffic': round(d['fabric_kb_per_launch'] * 1024 * launch_chain_steps /
+                                     (d['chains'] * d['steps_per_chain'])),
+                    'traffic_unit': 'bytes per launch (PMC FETCH_SIZE x 2 + WRITE_SIZE, scaled)',
+                    'valu_per_update': d['valu_per_update'], 'fp64_valu_per_update': d['fp64_valu_per_update'],
+                    'valu_pipe_cycles_per_update': cyc, 'wave_cycle_split': d['wave_cycle_split'],
+                    'pmc_source': d.get('source')})
+    return out
+
+
 def mh_cpu_baseline(P, budget_s=12.0):
     """oracle/mh_ref.c (C restatement, OpenMP over chains) on a bounded sample."""
     from oracle import mh_c
@@ -431,7 +466,6 @@ def main_mh(args):
     if rank == 0:
         steps = world * n * (iters + tune)
         value = steps / elapsed
-        flops = steps * 96 * MH_FP64_FLOP_PER_UPDATE / elapsed / 1e12
         line = {
             'metric': 'MH chain-steps/sec (48-ROI SRTM2, element-wise Metropolis)', 'value': round(value, 1),
             'unit': 'chain-steps/s', 'n_gpus': world, 'steps': 1, 'warmup': 1,
@@ -439,9 +473,7 @@ def main_mh(args):
             'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic (SRTM2 TAC + noise model, reference prior prior_stats_nROI48)',
             'config': {'workload': 'mcmc.py Metropolis-Hastings, 48 ROI x 2 params, SRTM2', 'chains_per_gpu': n,
                        'steps_per_chain': iters + tune, 'tune': tune},
-            'roofline': {'bound': 'valu-fp64', 'achieved': round(flops, 2), 'peak': 78.6, 'unit': 'TFLOP/s',
-                         'frac': round(flops / 78.6, 4), 'traffic': None,
-                         'flop_per_update': MH_FP64_FLOP_PER_UPDATE},
+            'roofline': mh_roofline(steps / elapsed / world, n * (iters + tune)),
             'mean_accept_rate': round(float(res['accept_rate'].mean()), 4),
             'reference_protocol_per_tac_s': round(ref_protocol_s, 2),
         }
@@ -663,8 +695,7 @@ def mh_config2_and_protocol(iddpm_10k_s, dev, cpu=True):
         cpu_proto = (time.perf_counter() - t2) * 10
     cfg2 = {'value': round(steps / el, 1), 'unit': 'chain-steps/s', 'chains': n, 'steps_per_chain': tune + draws,
             'tune': tune, 'draws': draws, 'seconds': round(el, 3), 'dtype': 'f64',
-            'roofline': {'bound': 'valu-fp64', 'achieved': round(fl, 2), 'peak': 78.6, 'unit': 'TFLOP/s',
-                         'frac': round(fl / 78.6, 4), 'traffic': None, 'flop_per_update': MH_FP64_FLOP_PER_UPDATE},
+            'roofline': mh_roofline(steps / el, steps),
             'mean_accept_rate': round(float(res['accept_rate'].mean()), 4),
             'cpu_baseline': mh_cpu_baseline(P) if cpu else None}
     return (cfg2,

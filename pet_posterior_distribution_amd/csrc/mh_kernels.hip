@@ -62,6 +62,31 @@ __device__ __forceinline__ double rsq_f64(double x) {
   return y;
 }
 
+// Round 6: e^x of the per-frame exponentials from a 64-entry table of 2^(j/64) in LDS: x = (64 m + j) ln 2 / 64 + r,
+// |r| <= ln 2 / 128, e^r by its degree-5 Taylor polynomial (truncation 3e-17), 2^m by ldexp (<= 2 ulp); about
+// 16 instructions and one LDS read against ocml's ~30.  Outside (-708, 709) and NaN: ocml's exp.  0: ocml's exp
+#ifndef MH_TEXP
+#define MH_TEXP 1
+#endif
+constexpr int kE2 = 64;
+__device__ __forceinline__ double exp_tab(const double* E2, double x) {
+  if (!(x > -708.0 && x < 709.0)) return exp(x);
+  const double kf = rint(x * 92.332482616893656);                 // 64 / ln 2
+  double r = fma(-kf, 6.93147180369123816490e-01 / 64, x);       // fdlibm's ln 2 split (kf ln2_hi exact), / 64
+  r = fma(-kf, 1.90821492927058770002e-10 / 64, r);
+  const int k = (int)kf, j = k & (kE2 - 1), m = k >> 6;
+  double q = 8.3333333333333333e-03;                              // 1/5!
+  q = fma(q, r, 4.1666666666666667e-02);
+  q = fma(q, r, 1.6666666666666667e-01);
+  q = fma(q, r, 0.5);
+  q = fma(q, r, 1.0);
+  q = fma(q, r, 1.0);
+  return ldexp(E2[j] * q, m);
+}
+__device__ __forceinline__ void load_e2(double* E2) {
+  for (int j = threadIdx.x; j < kE2; j += blockDim.x) E2[j] = exp2((double)j / kE2);
+}
+
 // e^{-k2a t} of the update kernel by fp64_math.h exp_fast (<= 1 ulp) instead of ocml's exp
 #ifndef MH_FAST_EXP
 #define MH_FAST_EXP 0
@@ -76,12 +101,12 @@ __device__ __forceinline__ double rsq_f64(double x) {
 // frame) by 8; the terms move by an ulp or two, so accept / reject paths can differ from the oracles' only
 // where log u lies within ~1e-15 of the ratio.  0: sqrt and divide (the oracles' expression order)
 #ifndef MH_RSQ
-#define MH_RSQ 0
+#define MH_RSQ 1
 #endif
 // Round 6: the sweep's per-element LDS operands (the next element's index, proposal draw, log u and prior
 // diagonal) read one element ahead, so their LDS round trips overlap the current element's likelihood
 #ifndef MH_PF
-#define MH_PF 0
+#define MH_PF 1
 #endif
 
 // LDS copy of the coefficient table (one element per thread)
@@ -105,6 +130,7 @@ struct Lds {
   double CR[NF], TV[NF];
   double MUD[NR], MUR[NR];
   alignas(16) double LPHI[LPNI * LPLD];   // log Phi polynomial (16-B aligned rows)
+  double E2[kE2];                         // 2^(j/64) (MH_TEXP)
   double E[kWaves][64];               // per-wave exponential scratch
   double Z[kWaves][2 * NR];           // per-wave sweep draws: N(0,1) proposal per element
   double LU[kWaves][2 * NR];          //   log accept-uniform per element
@@ -177,7 +203,7 @@ __device__ __forceinline__ double roi_loglik(const Lds& s, const double2 (&mreg)
   e[lane] = lane < NF ? 1.0 - k2a * s.TV[lane < NF ? lane : 0] : 0.0;
 #else
   const double ex = -k2a * s.TV[lane < NF ? lane : 0];
-  e[lane] = lane < NF ? (MH_FAST_EXP ? exp_fast(ex) : exp(ex)) : 0.0;   // e[54..63] = 0 (row padding)
+  e[lane] = lane < NF ? (MH_TEXP ? exp_tab(s.E2, ex) : MH_FAST_EXP ? exp_fast(ex) : exp(ex)) : 0.0;   // e[54..63] = 0
 #endif
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -240,6 +266,7 @@ __device__ void load_lds(Lds& s, const MHConst& c) {
   for (int k = threadIdx.x; k < NF; k += blockDim.x) { s.CR[k] = c.CR[k]; s.TV[k] = c.TV[k]; }
   for (int k = threadIdx.x; k < NR; k += blockDim.x) { s.MUD[k] = c.MUD[k]; s.MUR[k] = c.MUR[k]; }
   load_logphi(s.LPHI);
+  load_e2(s.E2);
   __syncthreads();
 }
 
@@ -508,6 +535,7 @@ struct LdsB {
   double CR[NF], TV[NF];
   double MUD[NR], MUR[NR];
   alignas(16) double LPHI[LPNI * LPLD];   // log Phi polynomial (16-B aligned rows)
+  double E2[kE2];                         // 2^(j/64) (MH_TEXP)
   double W[kBW][kWD];                 // per wave: e rows [q][MLD] / frame terms [q][64] / sweep draws
   double P[kBW][kQ * 4];              // per wave: the batch's (R1, k2, k2a, roi)
   double LL[kBW][kNE];                // per chain group: the draw's evaluations
@@ -536,7 +564,9 @@ __device__ __forceinline__ void eval_batch(const LdsB& s, double* W, double* P, 
     const double tv = s.TV[f];
 #pragma unroll 1
     for (int q = 0; q < kQ; ++q)
-      W[q * MLD + lane] = lane < NF ? ((MH_BEXP & 2) ? 1.0 - P[q * 4 + 2] * tv : exp(-P[q * 4 + 2] * tv)) : 0.0;
+      W[q * MLD + lane] = lane < NF ? ((MH_BEXP & 2) ? 1.0 - P[q * 4 + 2] * tv
+                                                     : MH_TEXP ? exp_tab(s.E2, -P[q * 4 + 2] * tv) : exp(-P[q * 4 + 2] * tv))
+                                    : 0.0;
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -627,6 +657,7 @@ __global__ __launch_bounds__(kBW * 64) void mh_chain_batched(MHConst c, MHRun r)
   for (int k = threadIdx.x; k < NF; k += blockDim.x) { s.CR[k] = c.CR[k]; s.TV[k] = c.TV[k]; }
   for (int k = threadIdx.x; k < NR; k += blockDim.x) { s.MUD[k] = c.MUD[k]; s.MUR[k] = c.MUR[k]; }
   load_logphi(s.LPHI);
+  load_e2(s.E2);
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int grp = w / WPC, rk = w - grp * WPC;

@@ -30,6 +30,12 @@ def largest_dispatch(path):
     return per[max(per, key=lambda d: (grid[d], d))]
 
 
+def kernel_hash():
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from pet_posterior_distribution_amd import _lib
+    return _lib.kernel_code_hash(b'mh_chain_kernel')
+
+
 def main():
     root, chains, steps, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
     c = {}
@@ -49,10 +55,10 @@ def main():
         'wave_cycle_split': {'issuing': round(c.get('SQ_ACTIVE_INST_ANY', 0) / wave, 4),
                              'waiting (s_waitcnt / barrier)': round(c.get('SQ_WAIT_ANY', 0) / wave, 4),
                              'issue-stalled': round(c.get('SQ_WAIT_INST_ANY', 0) / wave, 4)} if wave else None,
-        'clock_ghz_grbm': None,
         'lds_bank_conflict_per_update': round(f.get('SQ_LDS_BANK_CONFLICT', 0.0), 3),
         'fabric_kb_per_launch': round((2 * c.get('FETCH_SIZE', 0.0) + c.get('WRITE_SIZE', 0.0)), 1),
         'source': root,
+        'code_hash': kernel_hash(),
     }
     with open(out, 'w') as fo:
         json.dump(res, fo, indent=1)
