@@ -341,7 +341,14 @@ template <> struct LayerShape<LK_UP2_F> { static constexpr int L = 48, TAPS = 6,
 template <> struct LayerShape<LK_UP2_FX3> : LayerShape<LK_UP2_F> {};
 
 // launch-bound threads: 8 waves (4 MFMA + 4 loader) or 4 (fused layers)
-template <int KIND> constexpr int conv_max_threads() { return is_fused_kind(KIND) ? kThreads : 2 * kThreads; }
+// Round 6: the 16-bit fused final level (3-stage ring) with 4 loader waves issuing its LDS-DMA, as the down
+// layers (CONV_LOADERS): 512 threads, 256 registers a lane.  0: 4 waves that issue their own DMA
+#ifndef CONV_FIN_LDR
+#define CONV_FIN_LDR 0
+#endif
+template <int KIND> constexpr int conv_max_threads() {
+  return (CONV_FIN_LDR && CONV_LOADERS && KIND == LK_UP2_F) ? 2 * kThreads : is_fused_kind(KIND) ? kThreads : 2 * kThreads;
+}
 
 template <typename T, int KIND>
 struct ConvGeom {
@@ -490,23 +497,27 @@ struct ConvGeom {
   static constexpr int FMAP_OFF = (SMEM0 + 15) / 16 * 16;
   static constexpr int FMAP_BYTES = FIN_LDS ? (FMAP_FULL * kThreads + (FMAP_REM + 63) / 64 * 64) * 16 : 0;
   static constexpr int SMEM1 = SMEM0 > TAIL ? SMEM0 : TAIL;
-  static constexpr int SMEM = FIN_MAPS ? FMAP_OFF + FMAP_BYTES : SMEM1;
-  // fused final level (CONV_FIN_REGMAPS): the tile's map rows tmap[t] + cmap[tac] as [L][FIN_LD] fp32 and the
-  // final kernel wf4 [128][4], loaded to registers by every thread during the K loop's second-to-last chunk and
-  // written to LDS after the loop, past the transposed epilogue's partials / down0 maps (24 KB) and x_next rows
+  // fused final level (CONV_FIN_REGMAPS): the tile's map rows as [S][L][FIN_LD] fp32 -- tmap[t] + cmap[tac]
+  // of each sample, or one [L][FIN_LD] block when every sample shares them (t uniform and the handle's
+  // combined table: loaded to registers by every thread during the K loop's second-to-last chunk) -- and the
+  // final kernel wf4 [128][4], written to LDS after the loop, past the transposed epilogue's partials / down0
+  // maps (24 KB) and x_next rows
   static constexpr int FRM_PIECES = L * (NT / 4);               // 16-B pieces of one map (6 per thread)
   static constexpr int FRM_PT = FRM_PIECES / kThreads;
   static constexpr int FRM_OFF = 26 * 1024;
-  static constexpr int FRW_OFF = FRM_OFF + L * FIN_LD * 4;
-  static_assert(!FIN_MAPS || (FRM_PIECES % kThreads == 0 && FRW_OFF + 128 * 16 <= SMEM &&
-                              FRM_OFF >= 48 * 128 * 4 + MT * 2 * 4 + 64), "final-level map rows in LDS");
+  static constexpr int FRW_OFF = FRM_OFF + S * L * FIN_LD * 4;
+  static constexpr int FREND = FIN_MAPS ? FRW_OFF + 128 * 16 : 0;
+  static constexpr int SMEM2 = FIN_MAPS ? FMAP_OFF + FMAP_BYTES : SMEM1;
+  static constexpr int SMEM = SMEM2 > FREND ? SMEM2 : FREND;
+  static_assert(!FIN_MAPS || (FRM_PIECES % kThreads == 0 && FRM_OFF >= 48 * 128 * 4 + MT * 2 * 4 + 64),
+                "final-level map rows in LDS");
   static_assert(!FIN_MAPS || (TAIL == 0 && FIN_LD == 132 && NT == 128), "final map layout");
   static_assert(!PREMAP || EPI_BYTES <= MAP_OFF, "C tile must not overlap the prefetched maps");
   // Dedicated loader waves (16-bit 3-stage layers): 4 extra waves issue every LDS-DMA
   // piece, so the 4 MFMA waves never stall on DMA issue.
   // (not the fused layers: 4 waves per workgroup leave them the whole 512-entry register file
   // for the second segment's offsets and the correction weights)
-  static constexpr bool LDR = CONV_LOADERS && sizeof(T) == 2 && STAGES == 3 && !FUSED;
+  static constexpr bool LDR = CONV_LOADERS && sizeof(T) == 2 && STAGES == 3 && (!FUSED || (CONV_FIN_LDR && EPI == EPI_FINAL));
   static constexpr int NTH = LDR ? 2 * kThreads : kThreads;
   static_assert(WM * WN == 4, "4 waves");
   static_assert(!PM || (((S == 64 && L == 6) || (S == 32 && L == 12)) && WM == 4 && WN == 1 && !UPS && !FUSED),
@@ -959,8 +970,12 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   // ring's counted waits retire them for free, and the row loop after the K loop waits on LDS only
   // (a dependent global load there cost a full memory round trip per row).
   const FinalArgs& fa = a.fin;
-  const int s_me = tid / L, l_me = tid - s_me * L, b_me = m0 + s_me;
-  const bool row_ok = EPI == EPI_FINAL && tid < G::MT && b_me < B;
+  // loader-wave final level (FLDR): the loader waves run the epilogue's tail -- the p_sample rows and the
+  // next-step down0 -- as "row threads" rtid = tid - 256, the MFMA waves its head (the transposed final conv)
+  constexpr bool FLDR = G::LDR && EPI == EPI_FINAL;
+  const int rtid = FLDR ? (tid >= kThreads ? tid - kThreads : G::MT) : tid;
+  const int s_me = rtid / L, l_me = rtid - s_me * L, b_me = m0 + s_me;
+  const bool row_ok = EPI == EPI_FINAL && rtid < G::MT && b_me < B;
   const int bq = row_ok ? b_me : m0;
   const bool do_ps = fa.net_out == nullptr;
   int t_me = 0, tac_me = 0;
@@ -968,26 +983,35 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
   float bfin[4] = {0.f, 0.f, 0.f, 0.f}, xt_me[2] = {0.f, 0.f}, z_me[2] = {0.f, 0.f};
   PCoef pc{};
   unsigned long long rng0 = 0, rng1 = 0;
-  if constexpr (EPI == EPI_FINAL) {
-    static_assert(EPI != EPI_FINAL || G::MT <= kThreads, "one final row per thread");
-    t_me = a.t_uniform >= 0 ? a.t_uniform : a.tvec[bq];
-    tac_me = a.tac ? a.tac[bq] : 0;
-    idx_me = ((size_t)bq * L + (row_ok ? l_me : 0)) * 2;
+  auto load_final_operands = [&]() {
+    if constexpr (EPI == EPI_FINAL) {
+      static_assert(EPI != EPI_FINAL || G::MT <= kThreads, "one final row per thread");
+      // (every operand (re)defined here: the zeros above must not stay live across the K loop)
+      xt_me[0] = xt_me[1] = z_me[0] = z_me[1] = 0.f;
+      rng0 = rng1 = 0;
+      pc = PCoef{};
+      t_me = a.t_uniform >= 0 ? a.t_uniform : a.tvec[bq];
+      tac_me = a.tac ? a.tac[bq] : 0;
+      idx_me = ((size_t)bq * L + (row_ok ? l_me : 0)) * 2;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) bfin[q] = q < fa.n_out ? fa.bf[q] : 0.f;
-    if (do_ps) {
-      xt_me[0] = fa.x_t[idx_me];
-      xt_me[1] = fa.x_t[idx_me + 1];
-      if (fa.z) {
-        z_me[0] = fa.z[idx_me];
-        z_me[1] = fa.z[idx_me + 1];
-      } else {
-        rng0 = fa.rng[0];
-        rng1 = fa.rng[1];
+      for (int q = 0; q < 4; ++q) bfin[q] = q < fa.n_out ? fa.bf[q] : 0.f;
+      if (do_ps) {
+        xt_me[0] = fa.x_t[idx_me];
+        xt_me[1] = fa.x_t[idx_me + 1];
+        if (fa.z) {
+          z_me[0] = fa.z[idx_me];
+          z_me[1] = fa.z[idx_me + 1];
+        } else {
+          rng0 = fa.rng[0];
+          rng1 = fa.rng[1];
+        }
+        pc = load_pcoef(fa, t_me);
       }
-      pc = load_pcoef(fa, t_me);
     }
-  }
+  };
+  // (the loader-wave final level loads them after its K loop, where 256 registers a lane cannot keep them
+  // live across the loop: they land behind the transposed final conv)
+  if constexpr (!G::LDR) load_final_operands();
 
   // zero row of every stage
   if (tid < G::STAGES * G::CPR) {
@@ -2052,7 +2076,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     // compute has its own and its DMA target's segment at compile time, so no loop body
     // branches on the segment.  Host guarantees n1 >= 3 (3-stage) / >= 1 and n2 >= 2.
     const int n1 = dma.n1;
-    if (has_m0) load_epk(0);   // the first segment-2 chunk's correction weights
+    if (has_m0 && !loader) load_epk(0);   // the first segment-2 chunk's correction weights
     if constexpr (G::STAGES == 2) {
       dma.all(smem, 0, 0, lane);
       prefetch_maps();
@@ -2075,6 +2099,44 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       fin_reg_issue();   // (lands during the last chunk)
       compute(smem + (kc & 1) * G::STAGE, No{}, 0, 0, Seg2{}, kc, P0{});
       __syncthreads();
+    } else if constexpr (G::LDR) {
+      // loader-wave final level (CONV_FIN_LDR): waves 4..7 issue every LDS-DMA piece (chunk c lands in stage
+      // c % 3; chunk c + 3 goes into stage c % 3 after barrier B(c + 1), when the MFMA waves are done with
+      // chunk c), the MFMA waves compute one chunk per barrier.  Both sides pass B0 + NC barriers.
+      if (loader) {
+        dma.all(smem, 0, 0, lane);
+        ring_barrier<0>();                                   // B0: chunk 0 landed
+        if (NC > 1) dma.all(smem, 1, 1, lane);
+        if (NC > 2) dma.all(smem, 2, 2, lane);
+        for (int kc = 0; kc < NC; ++kc) {
+          // B(kc + 1): chunk kc + 1 landed; chunk kc + 2 (its segment's piece count) may still be in flight
+          if (kc + 2 < NC) {
+            if (kc + 2 >= n1) ring_barrier<G::PER2>();
+            else ring_barrier<G::PER>();
+          } else {
+            ring_barrier<0>();
+          }
+          if (kc + 3 < NC) dma.all(smem, kc + 3, kc % 3, lane);
+        }
+      } else {
+        ring_barrier<0>();                                   // B0
+#if CONV_EXP_MODE & 128
+        st_c0 = __builtin_amdgcn_s_memtime();
+        st_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+        int buf = 0, kc = 0;
+        for (; kc < n1; ++kc) {
+          compute(smem + buf * G::STAGE, No{}, 0, 0, Seg1{}, 0, P0{});
+          ring_barrier<0>();                                 // B(kc + 1)
+          buf = buf == 2 ? 0 : buf + 1;
+        }
+        for (; kc < NC; ++kc) {
+          if (kc == NC - 2) fin_reg_issue();                 // (lands during chunk NC - 2)
+          compute(smem + buf * G::STAGE, No{}, 0, 0, Seg2{}, kc, P0{});
+          ring_barrier<0>();
+          buf = buf == 2 ? 0 : buf + 1;
+        }
+      }
     } else {
       dma.all(smem, 0, 0, lane);
       prefetch_maps();
@@ -2355,7 +2417,8 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     }
   }
   }
-  if (loader) return;   // s_barrier waits only for the waves still running
+  if (loader && !FLDR) return;   // s_barrier waits only for the waves still running
+  if (!loader) {   // (FLDR: the loader waves go on to the epilogue's tail)
   if constexpr (G::PM || G::W6) {
     // flushed at the end of the position-major / zero-skip main loop
   } else if constexpr (UC && M16) {   // the last chunk's last step: composite tap 3, keys 2 i + rh + 3
@@ -2381,6 +2444,7 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         if constexpr (!(CONV_EXP_MODE & 2)) acc[i][jn] = mfma32(uca[HL][2 * i + G::TAPS2 - 1], bv[1][jn], acc[i][jn]);
   } else {
     mfma_bf16(1);   // the last chunk's last step (NS even)
+  }
   }
 #if CONV_EXP_MODE & 128
   {   // diagnostic: main-loop cycles and the clock (s_memrealtime = 100 MHz)
@@ -2603,6 +2667,9 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     // channels wn * 64 + jn * 32 + 8 g + 4 h + q (register 4 g + q); it adds the map rows, applies the
     // relu and dots its 32 channels with wf4 in registers -- no C-tile staging -- and the four
     // (wn, h) partial sums of a row meet in LDS [4][MT][4].
+    if constexpr (FLDR) {
+      if (loader) load_final_operands();
+    }
     float* fin = reinterpret_cast<float*>(smem);
     // TF: the partials [4][MT][4] and, after the row loop, the fused down0's map rows [48][128] share fin
     static_assert(!TF || 4 * G::MT * 4 <= 48 * 128, "TF partials inside the down0 map region");
@@ -2618,60 +2685,68 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       // loaded during the K loop
       float* frl = reinterpret_cast<float*>(smem + G::FRM_OFF);
       if (fin_reg) {
+        if (!loader) {
 #pragma unroll
-        for (int k = 0; k < G::FRM_PT; ++k) {
-          const int q = tid + kThreads * k, l = q / (NT / 4), c = q - l * (NT / 4);
-          *reinterpret_cast<f32x4*>(frl + l * G::FIN_LD + 4 * c) = frm[k];
+          for (int k = 0; k < G::FRM_PT; ++k) {
+            const int q = tid + kThreads * k, l = q / (NT / 4), c = q - l * (NT / 4);
+            *reinterpret_cast<f32x4*>(frl + l * G::FIN_LD + 4 * c) = frm[k];
+          }
+        }
+      } else {   // per-sample t or conditions: each sample's rows tmap[t_s] + cmap[tac_s], staged by every thread
+#pragma unroll 4
+        for (int q = tid; q < G::S * G::FRM_PIECES; q += G::NTH) {
+          const int sl = q / (NT / 4), c = q - sl * (NT / 4), sq = sl / L, l = sl - sq * L;
+          const int b = min(m0 + sq, B - 1);     // absent samples: finite values, never stored
+          const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[b];
+          f32x4 v = *reinterpret_cast<const f32x4*>(a.tmap + ((size_t)t * L + l) * cout + 4 * c);
+          if (a.cmap) v += *reinterpret_cast<const f32x4*>(a.cmap + ((size_t)(a.tac ? a.tac[b] : 0) * L + l) * cout + 4 * c);
+          *reinterpret_cast<f32x4*>(frl + sl * G::FIN_LD + 4 * c) = v;
         }
       }
       if (tid < 128) *reinterpret_cast<f32x4*>(smem + G::FRW_OFF + 16 * tid) = frw;
       __syncthreads();
+      if (!loader) {   // (FLDR: the MFMA waves; the loader waves hold no accumulators)
       const float* wfs = reinterpret_cast<const float*>(smem + G::FRW_OFF);
       // per row: o4 accumulates over (jn, g, q) in the same order as the register-wq loop below (bitwise equal)
       f32x4 o3[3] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-      const float* mrow[3][2];
+      // one (jn, g) step: the lane's 4 channels n .. n + 3 of its 3 rows (hv: their map values)
+      auto tf_step = [&](int jn, int g, const f32x4 (&hv)[3]) {
+        const int n = wn * 64 + jn * 32 + 8 * g + 4 * h;
+        f32x4 wq4[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) wq4[q] = *reinterpret_cast<const f32x4*>(wfs + (n + q) * 4);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float hq = fmaxf(acc[i][jn][4 * g + q] + hv[i][q], 0.f);
+            o3[i][0] = fmaf(hq, wq4[q][0], o3[i][0]);
+            o3[i][1] = fmaf(hq, wq4[q][1], o3[i][1]);
+            o3[i][2] = fmaf(hq, wq4[q][2], o3[i][2]);
+            o3[i][3] = fmaf(hq, wq4[q][3], o3[i][3]);
+          }
+      };
+      int mrow[3];                               // the LDS map row of each of the lane's 3 tile rows
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
-        const int r = wm * 96 + 32 * i + lr;
-        int sr, lr_;
-        G::row_sl(r, sr, lr_);
-        const int br = min(m0 + sr, B - 1);
-        if (fin_reg) {
-          mrow[i][0] = frl + lr_ * G::FIN_LD;
-          mrow[i][1] = nullptr;
-        } else {
-          const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[br];
-          const int tac = a.tac ? a.tac[br] : 0;
-          mrow[i][0] = a.tmap + ((size_t)t * L + lr_) * cout;
-          mrow[i][1] = a.cmap ? a.cmap + ((size_t)tac * L + lr_) * cout : nullptr;   // (null: combined table)
-        }
+        int sr, lq;
+        G::row_sl(wm * 96 + 32 * i + lr, sr, lq);
+        mrow[i] = ((fin_reg ? 0 : sr) * L + lq) * G::FIN_LD;
       }
 #pragma unroll
       for (int jn = 0; jn < 2; ++jn)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int n = wn * 64 + jn * 32 + 8 * g + 4 * h;
-          f32x4 wq4[4];
+          f32x4 hv[3];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) wq4[q] = *reinterpret_cast<const f32x4*>(wfs + (n + q) * 4);
-#pragma unroll
-          for (int i = 0; i < 3; ++i) {
-            const f32x4 hv = (fin_reg || !mrow[i][1]) ? *reinterpret_cast<const f32x4*>(mrow[i][0] + n)
-                                                      : *reinterpret_cast<const f32x4*>(mrow[i][0] + n) +
-                                                            *reinterpret_cast<const f32x4*>(mrow[i][1] + n);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const float hq = fmaxf(acc[i][jn][4 * g + q] + hv[q], 0.f);
-              o3[i][0] = fmaf(hq, wq4[q][0], o3[i][0]);
-              o3[i][1] = fmaf(hq, wq4[q][1], o3[i][1]);
-              o3[i][2] = fmaf(hq, wq4[q][2], o3[i][2]);
-              o3[i][3] = fmaf(hq, wq4[q][3], o3[i][3]);
-            }
-          }
+          for (int i = 0; i < 3; ++i) hv[i] = *reinterpret_cast<const f32x4*>(frl + mrow[i] + n);
+          tf_step(jn, g, hv);
         }
 #pragma unroll
       for (int i = 0; i < 3; ++i)
         *reinterpret_cast<f32x4*>(fin + ((wn * 2 + h) * G::MT + wm * 96 + 32 * i + lr) * 4) = o3[i];
+      }
 #else
       f32x4 wq[2][4][4];                              // wf4 rows of this lane's 32 channels
 #pragma unroll
@@ -2739,19 +2814,21 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     // registers here so their latency hides behind the row loop below (issued before the TF final
     // conv instead they measured slower: up2 39.7 vs 38.5-38.8 us, profiles/r04/ab_r4d/ab_tf_early_*).
     static_assert(G::MT % L == 0 && L == 48, "fused down0 needs whole 48-ROI samples");
-    static_assert(G::NTH == kThreads, "fused down0 strides assume one 256-thread block");
+    // (FLDR: the 256 row threads of the tail are the loader waves, rtid = tid - 256)
+    static_assert(G::NTH == kThreads || FLDR, "fused down0 strides assume one 256-thread block");
     const Down0Args& nd = f.next;
     const int nb_next = min(G::MT / L, B - m0);
-    const int n0_next = (tid & 15) * 8;
+    const int n0_next = (rtid & 15) * 8;
     int* flag = reinterpret_cast<int*>(xst + G::MT * 2);
     f32x4 wr[12][2], mv[6];
-    if (fuse_next) {
+    const bool tail = !FLDR || loader;
+    if (fuse_next && tail) {
       const int tac0 = nd.tac ? nd.tac[m0] : 0;
       // one condition in the tile?  Wave 0 votes (nb <= 64); no __syncthreads_and, whose
       // LDS scratch costs the K loop its counted LDS-DMA waits (vmcnt(0) per read group).
-      if (tid < 64) {
-        const unsigned long long ok = __ballot(!nd.tac || tid >= nb_next || nd.tac[m0 + tid] == tac0);
-        if (tid == 0) *flag = ok == ~0ull;
+      if (rtid < 64) {
+        const unsigned long long ok = __ballot(!nd.tac || rtid >= nb_next || nd.tac[m0 + rtid] == tac0);
+        if (rtid == 0) *flag = ok == ~0ull;
       }
 #pragma unroll
       for (int jc = 0; jc < 12; ++jc) {
@@ -2761,17 +2838,20 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       const f32x4* tm = reinterpret_cast<const f32x4*>(nd.tmap + (size_t)nd.t_uniform * 48 * 128);
       const f32x4* cm = reinterpret_cast<const f32x4*>(nd.cmap + (size_t)tac0 * 48 * 128);
 #pragma unroll
-      for (int k = 0; k < 6; ++k) mv[k] = tm[tid + kThreads * k] + cm[tid + kThreads * k];
+      for (int k = 0; k < 6; ++k) mv[k] = tm[rtid + kThreads * k] + cm[rtid + kThreads * k];
     }
     __syncthreads();
+    if constexpr (FLDR) {
+      if (!loader) return;   // the MFMA waves are done: their partial sums are in LDS
+    }
 #if CONV_EXP_MODE & 128
-    if (tid == 0) reinterpret_cast<unsigned long long*>(a.fin.x_all)[4096 + 2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    if (rtid == 0) reinterpret_cast<unsigned long long*>(a.fin.x_all)[4096 + 2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 #endif
     // one Philox call yields the Box-Muller pair for both parameters of this ROI (its key landed
     // during the staging above; pure ALU from here)
     if (do_ps && !f.z && row_ok) philox_normal2(rng0, rng1 + (unsigned long long)b_me, f.rng_step, l_me, z_me);
     if (row_ok) {
-      const int r = tid, l = l_me, b = b_me, t = t_me, tac = tac_me;
+      const int r = rtid, l = l_me, b = b_me, t = t_me, tac = tac_me;
       if constexpr ((FIN_EXP & 4) != 0) { xst[r * 2] = xst[r * 2 + 1] = fin[r * G::FIN_LD]; goto fin_rows_done; }
       const float* mp = a.tmap ? a.tmap + ((size_t)t * L + l) * cout : nullptr;
       const float* cp = a.cmap ? a.cmap + ((size_t)tac * L + l) * cout : nullptr;
@@ -2837,20 +2917,20 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
       // same per-position code as down0_kernel, 16 positions in flight per pass.
       __syncthreads();                               // x_next rows staged; C tile dead
 #if CONV_EXP_MODE & 128
-      if (tid == 0) reinterpret_cast<unsigned long long*>(a.fin.x_all)[4096 + 2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+      if (rtid == 0) reinterpret_cast<unsigned long long*>(a.fin.x_all)[4096 + 2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
 #endif
       const bool fast = *flag != 0;
       float* mp = fin;
       if (fast) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) reinterpret_cast<f32x4*>(mp)[tid + kThreads * k] = mv[k];
+        for (int k = 0; k < 6; ++k) reinterpret_cast<f32x4*>(mp)[rtid + kThreads * k] = mv[k];
       }
       __syncthreads();
-      if constexpr (!(FIN_EXP & 1)) down0_positions<T, XS>(nd, xst, mp, fast, m0, nb_next, wr, n0_next, tid >> 4, kThreads / 16);
+      if constexpr (!(FIN_EXP & 1)) down0_positions<T, XS>(nd, xst, mp, fast, m0, nb_next, wr, n0_next, rtid >> 4, kThreads / 16);
 #if CONV_EXP_MODE & 128
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (tid == 0) reinterpret_cast<unsigned long long*>(a.fin.x_all)[8192 + 4 * blockIdx.x + 3] = __builtin_amdgcn_s_memrealtime();
+      if (rtid == 0) reinterpret_cast<unsigned long long*>(a.fin.x_all)[8192 + 4 * blockIdx.x + 3] = __builtin_amdgcn_s_memrealtime();
 #endif
     }
   }
