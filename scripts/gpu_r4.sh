@@ -89,6 +89,8 @@ if has mhpmc; then
     i=$((i+1))
     timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $CTR -d $GRAFT_REPO_ROOT/$OUT/mhpmc/p$i -o run --output-format csv -- $MHAPP > $OUT/mhpmc_p$i.log 2>&1 || { echo "mh pmc pass $i failed"; tail -5 $OUT/mhpmc_p$i.log; exit 1; }
   done
+  python scripts/mh_pmc_summary.py $OUT/mhpmc 10000 600 $OUT/mh_pmc.json > /dev/null || { echo "mh pmc summary failed"; exit 1; }
+  cp $OUT/mh_pmc.json profiles/mh_pmc.json   # (the bench stage below reads it)
   head -c 300 $OUT/mh_short.json; echo
 fi
 if has bench; then
