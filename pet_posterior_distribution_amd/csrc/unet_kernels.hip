@@ -897,6 +897,109 @@ __device__ __forceinline__ void down0_positions(const Down0Args& a, const float*
   }
 }
 
+// Round 6: down0 on the MFMA array for the 16-bit networks (CONV_DOWN0_MFMA).  For a group of 4 samples and the
+// 32-channel column block cb, the 96 (sample, pooled position lp) pairs form 3 row blocks of 32; each block
+// pair computes the even (l = 2 lp) and the odd (l = 2 lp + 1) positions of the same 32 pairs, so the max pool
+// is a register-wise max.  K = (tap j, x-channel c) = 2 j + c < 12 of 16 (zero-padded).  Operands split
+// hi + lo in bf16 as the bf16x3 network does: W x = Wh xh + Wl xh + Wh xl, fp32 accumulation (about 2^-16
+// relative, for every 16-bit network).  The MFMA runs transposed (weights as A, x as B), so lane (row rl,
+// half h) holds 16 channels 8 g + 4 h + q of its row; a lane pair exchanges quads (shfl_xor 32) so that each
+// lane stores two 16-B pieces of 8 consecutive channels.  w8: this lane's weights W[k = 8 h .. 8 h + 7][n].
+// xs [nb][96] fp32 in LDS; mp [48][128] (fast: t uniform, one condition) or the global maps per sample.
+template <typename T, int XS>
+__device__ __forceinline__ void down0_mfma(const Down0Args& a, const float* xs, const float* mp, bool fast, int b0,
+                                           int nb, int grp, int cb, int lane, const float (&w8)[8]) {
+  const int h = lane >> 5, rl = lane & 31;
+  bf16x8 wh, wl;
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    wh[kk] = (bf16)w8[kk];
+    wl[kk] = (bf16)(w8[kk] - (float)wh[kk]);
+  }
+#pragma unroll
+  for (int bp = 0; bp < 3; ++bp) {
+    const int P = 32 * bp + rl, sq = P / 24, lp = P - 24 * sq, sg = 4 * grp + sq;
+    const bool live = sg < nb;
+    const int b = b0 + (live ? sg : 0);
+    float v[2][16];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int l = 2 * lp + e;
+      bf16x8 xh, xl;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int p = l - 2 + 4 * h + jj;
+        const bool ok = live && p >= 0 && p < 48 && 4 * h + jj < 6;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const float x = ok ? xs[sg * 96 + p * 2 + c] : 0.f;
+          xh[2 * jj + c] = (bf16)x;
+          xl[2 * jj + c] = (bf16)(x - (float)xh[2 * jj + c]);
+        }
+      }
+      f32x16 acc = {};
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xh, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, xh, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xl, acc, 0, 0, 0);
+      const float* tmr = nullptr;
+      const float* cmr = nullptr;
+      if (!fast) {
+        const int tac = a.tac ? a.tac[b] : 0;
+        const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[b];
+        tmr = a.tmap + ((size_t)t * 48 + l) * 128;
+        cmr = a.cmap + ((size_t)tac * 48 + l) * 128;
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = 32 * cb + 8 * g + 4 * h;
+        const f32x4 m = fast ? *reinterpret_cast<const f32x4*>(mp + l * 128 + n)
+                             : *reinterpret_cast<const f32x4*>(tmr + n) + *reinterpret_cast<const f32x4*>(cmr + n);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[e][4 * g + q] = fmaxf(acc[4 * g + q] + m[q], 0.f);
+      }
+    }
+    // three rows to store: s0 (b, 2 lp), s0 (b, 2 lp + 1), p0 (b, lp)
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      float u[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) u[r] = o < 2 ? v[o][r] : fmaxf(v[0][r], v[1][r]);
+#pragma unroll
+      for (int gg = 0; gg < 2; ++gg) {
+        // this lane stores group g_own = 2 gg + h (channels 8 g_own .. + 7); the partner's half of it arrives
+        float send[4], st[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) send[q] = h ? u[4 * (2 * gg) + q] : u[4 * (2 * gg + 1) + q];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float recv = __shfl_xor(send[q], 32);
+          const float own = h ? u[4 * (2 * gg + 1) + q] : u[4 * (2 * gg) + q];
+          st[q] = h ? recv : own;
+          st[4 + q] = h ? own : recv;
+        }
+        if (live) {
+          const int n0 = 32 * cb + 8 * (2 * gg + h);
+          if constexpr (!(FIN_EXP & 2)) {
+            if (o < 2) store_act<T, XS>(reinterpret_cast<T*>(a.s0), (size_t)b * 48 + 2 * lp + o, 128, n0, st);
+            else store_act<T, XS>(reinterpret_cast<T*>(a.p0), (size_t)b * 24 + lp, 128, n0, st);
+          } else if (st[0] == 12345.f) {
+            reinterpret_cast<T*>(a.s0)[0] = (T)0.f;
+          }
+        }
+      }
+    }
+  }
+}
+// this lane's down0 weights for down0_mfma: W[k][n], k = 8 h .. 8 h + 7 (zero for k >= 12), n = 32 cb + lane % 32
+__device__ __forceinline__ void down0_mfma_weights(const float* w0, int cb, int lane, float (&w8)[8]) {
+  const int h = lane >> 5, n = 32 * cb + (lane & 31);
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) w8[kk] = 8 * h + kk < 12 ? w0[(8 * h + kk) * 128 + n] : 0.f;
+}
+#ifndef CONV_DOWN0_MFMA
+#define CONV_DOWN0_MFMA 0
+#endif
+
 // compile-time loop: f(integral_constant<int, I>) for I in [I0, N) (the step index of a fully unrolled main
 // loop whose register-array indices must fold; a #pragma unroll the compiler declines leaves them dynamic,
 // i.e. in scratch)
@@ -2820,7 +2923,9 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
     const int nb_next = min(G::MT / L, B - m0);
     const int n0_next = (rtid & 15) * 8;
     int* flag = reinterpret_cast<int*>(xst + G::MT * 2);
-    f32x4 wr[12][2], mv[6];
+    constexpr bool D0M = CONV_DOWN0_MFMA && sizeof(T) == 2;   // down0 on the MFMA array (down0_mfma)
+    f32x4 wr[D0M ? 1 : 12][2], mv[6];
+    float w8[8];
     const bool tail = !FLDR || loader;
     if (fuse_next && tail) {
       const int tac0 = nd.tac ? nd.tac[m0] : 0;
@@ -2830,10 +2935,14 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         const unsigned long long ok = __ballot(!nd.tac || rtid >= nb_next || nd.tac[m0 + rtid] == tac0);
         if (rtid == 0) *flag = ok == ~0ull;
       }
+      if constexpr (D0M) {
+        down0_mfma_weights(nd.w0, rtid >> 6, lane, w8);
+      } else {
 #pragma unroll
-      for (int jc = 0; jc < 12; ++jc) {
-        wr[jc][0] = *reinterpret_cast<const f32x4*>(nd.w0 + jc * 128 + n0_next);
-        wr[jc][1] = *reinterpret_cast<const f32x4*>(nd.w0 + jc * 128 + n0_next + 4);
+        for (int jc = 0; jc < 12; ++jc) {
+          wr[jc][0] = *reinterpret_cast<const f32x4*>(nd.w0 + jc * 128 + n0_next);
+          wr[jc][1] = *reinterpret_cast<const f32x4*>(nd.w0 + jc * 128 + n0_next + 4);
+        }
       }
       const f32x4* tm = reinterpret_cast<const f32x4*>(nd.tmap + (size_t)nd.t_uniform * 48 * 128);
       const f32x4* cm = reinterpret_cast<const f32x4*>(nd.cmap + (size_t)tac0 * 48 * 128);
@@ -2926,7 +3035,10 @@ __device__ __forceinline__ void conv_body(ConvArgs<T> a, char* smem, const int b
         for (int k = 0; k < 6; ++k) reinterpret_cast<f32x4*>(mp)[rtid + kThreads * k] = mv[k];
       }
       __syncthreads();
-      if constexpr (!(FIN_EXP & 1)) down0_positions<T, XS>(nd, xst, mp, fast, m0, nb_next, wr, n0_next, rtid >> 4, kThreads / 16);
+      if constexpr (!(FIN_EXP & 1)) {
+        if constexpr (D0M) down0_mfma<T, XS>(nd, xst, mp, fast, m0, nb_next, 0, rtid >> 6, lane, w8);
+        else down0_positions<T, XS>(nd, xst, mp, fast, m0, nb_next, wr, n0_next, rtid >> 4, kThreads / 16);
+      }
 #if CONV_EXP_MODE & 128
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -2963,11 +3075,18 @@ __global__ __launch_bounds__(512) void down0_kernel(Down0Args a, int spb) {
   bool fast = a.t_uniform >= 0;                   // t uniform and one condition in the block
   if (a.tac) fast = __syncthreads_and(fast && (tid >= nb || a.tac[b0 + tid] == tac0)) != 0;
   const int n0 = (tid & 15) * 8;
-  f32x4 wr[12][2];
+  constexpr bool D0M = CONV_DOWN0_MFMA && sizeof(T) == 2;   // the fused next-step down0's MFMA path (bitwise equal)
+  const int w = tid >> 6, lane = tid & 63;
+  f32x4 wr[D0M ? 1 : 12][2];
+  float w8[8];
+  if constexpr (D0M) {
+    down0_mfma_weights(a.w0, w & 3, lane, w8);
+  } else {
 #pragma unroll
-  for (int jc = 0; jc < 12; ++jc) {
-    wr[jc][0] = *reinterpret_cast<const f32x4*>(a.w0 + jc * 128 + n0);
-    wr[jc][1] = *reinterpret_cast<const f32x4*>(a.w0 + jc * 128 + n0 + 4);
+    for (int jc = 0; jc < 12; ++jc) {
+      wr[jc][0] = *reinterpret_cast<const f32x4*>(a.w0 + jc * 128 + n0);
+      wr[jc][1] = *reinterpret_cast<const f32x4*>(a.w0 + jc * 128 + n0 + 4);
+    }
   }
   const float xin = tid < nb * 96 ? a.x[(size_t)b0 * 96 + tid] : 0.f;   // nb * 96 <= 768: two passes
   const float xin2 = tid + 512 < nb * 96 ? a.x[(size_t)b0 * 96 + tid + 512] : 0.f;
@@ -2985,7 +3104,12 @@ __global__ __launch_bounds__(512) void down0_kernel(Down0Args a, int spb) {
     for (int k = 0; k < 3; ++k) reinterpret_cast<f32x4*>(mp)[tid + 512 * k] = mv[k];
   }
   __syncthreads();
-  down0_positions<T, XS>(a, xs, mp, fast, b0, nb, wr, n0, tid >> 4, 32);
+  if constexpr (D0M) {
+    // 8 waves: 4-sample group w / 4 (spb <= 8), column block w % 4
+    if (4 * (w >> 2) < nb) down0_mfma<T, XS>(a, xs, mp, fast, b0, nb, w >> 2, w & 3, lane, w8);
+  } else {
+    down0_positions<T, XS>(a, xs, mp, fast, b0, nb, wr, n0, tid >> 4, 32);
+  }
 }
 
 // ---------------------------------------------------------------------------
