@@ -34,6 +34,9 @@ constexpr int LPNI = PETMH_LOGPHI_NI, LPLD = 18;   // LDS row: 16 coefficients (
 static_assert(PETMH_LOGPHI_DEG == 14, "8 x 16-B pieces per row");   // 144-B rows: conflict-free ds_read_b128
 __constant__ double c_logphi[LPNI][PETMH_LOGPHI_DEG + 1] = PETMH_LOGPHI_COEF;
 
+#ifndef MH_ESTRIN
+#define MH_ESTRIN 0
+#endif
 // log Phi(x) for 0 <= x < 10 (x = NaN: NaN): interval k = floor(x), Horner in u = x - (k + 0.5)
 // from the LDS copy of the coefficients (row k: pieces (c_2j, c_2j+1)).
 __device__ __forceinline__ double log_phi_poly(const double* tab, double x) {
@@ -41,6 +44,16 @@ __device__ __forceinline__ double log_phi_poly(const double* tab, double x) {
   k = k < 0 ? 0 : (k > LPNI - 1 ? LPNI - 1 : k);
   const double u = x - ((double)k + 0.5);
   const double2* row = reinterpret_cast<const double2*>(tab + k * LPLD);
+#if MH_ESTRIN
+  // Estrin's scheme: depth 5 instead of Horner's 14 dependent FMAs (the update is latency-bound at 2 waves / SIMD)
+  double q[8];
+#pragma unroll
+  for (int j = 0; j < 7; ++j) q[j] = fma(row[j].y, u, row[j].x);
+  q[7] = row[7].x;
+  const double u2 = u * u, u4 = u2 * u2, u8 = u4 * u4;
+  const double r0 = fma(q[1], u2, q[0]), r1 = fma(q[3], u2, q[2]), r2 = fma(q[5], u2, q[4]), r3 = fma(q[7], u2, q[6]);
+  return fma(fma(r3, u4, r2), u8, fma(r1, u4, r0));
+#else
   double p = row[7].x;
 #pragma unroll
   for (int j = 6; j >= 0; --j) {
@@ -49,6 +62,7 @@ __device__ __forceinline__ double log_phi_poly(const double* tab, double x) {
     p = fma(p, u, cc.x);
   }
   return p;
+#endif
 }
 
 // 1/sqrt(x) for a positive normal x: v_rsq_f64, then two Newton steps y (1 + (1/2 - x y^2 / 2)) in fma form
@@ -107,6 +121,12 @@ __device__ __forceinline__ void load_e2(double* E2) {
 // diagonal) read one element ahead, so their LDS round trips overlap the current element's likelihood
 #ifndef MH_PF
 #define MH_PF 1
+#endif
+
+// Round 6: the update's operator matvec on DPP row broadcasts of e (conv_dpp) instead of an LDS round trip
+// of e (a write and 28 broadcast ds_read_b128, about three in flight).  0: the LDS matvec
+#ifndef MH_DPP
+#define MH_DPP 1
 #endif
 
 // LDS copy of the coefficient table (one element per thread)
@@ -195,7 +215,90 @@ __device__ __forceinline__ double log_ndtr(double x) {
 #ifndef MH_MROW_REG
 #define MH_MROW_REG 1
 #endif
-__device__ __forceinline__ double roi_loglik(const Lds& s, const double2 (&mreg)[MLD / 2], double* e, int lane, int i,
+#if MH_DPP
+// conv_f = sum_g M[f][g] e[g] with e[g] held by lane g, no LDS round trip: two permlane swaps replicate each
+// 16-lane row j of e into every row (X_j), and v_fmac_f64 with DPP row_newbcast:k hands every lane
+// e[16 j + k] as its first operand.  The lane's operator row M[f][0..53] lives in registers.
+using MRow = double[NF];
+template <int K, bool FIRST>
+__device__ __forceinline__ void fma_nb(double& acc, double x, double m) {
+  // FIRST: 2 wait states between the VALU write of x (the permlane swaps) and its DPP read
+  if constexpr (FIRST)
+    asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc) : "v"(x), "v"(m), "i"(K));
+  else
+    asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x), "v"(m), "i"(K));
+}
+template <int K>
+__device__ __forceinline__ void conv_terms(const MRow& mr, const double (&X)[4], double (&a)[4]) {
+  if constexpr (K < 16) {
+    fma_nb<K, K == 0>(a[0], X[0], mr[K]);
+    fma_nb<K, K == 0>(a[1], X[1], mr[16 + K]);
+    fma_nb<K, K == 0>(a[2], X[2], mr[32 + K]);
+    if constexpr (48 + K < NF) fma_nb<K, K == 0>(a[3], X[3], mr[48 + K]);
+    conv_terms<K + 1>(mr, X, a);
+  }
+}
+__device__ __forceinline__ double conv_dpp(const MRow& mr, double ev) {   // every lane active
+  const unsigned long long b = (unsigned long long)__double_as_longlong(ev);
+  const unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
+  // permlane16_swap(x, x): odd rows of the first copy <-> even rows of the second: {[E0 E0 E2 E2], [E1 E1 E3 E3]}
+  const auto l16 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h16 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  // permlane32_swap(y, y): rows 2-3 of the first copy <-> rows 0-1 of the second: {[Ea x4], [Eb x4]}
+  const auto l02 = __builtin_amdgcn_permlane32_swap(l16[0], l16[0], false, false);
+  const auto h02 = __builtin_amdgcn_permlane32_swap(h16[0], h16[0], false, false);
+  const auto l13 = __builtin_amdgcn_permlane32_swap(l16[1], l16[1], false, false);
+  const auto h13 = __builtin_amdgcn_permlane32_swap(h16[1], h16[1], false, false);
+  auto mk = [](unsigned l, unsigned h) { return __longlong_as_double((long long)(((unsigned long long)h << 32) | l)); };
+  const double X[4] = {mk(l02[0], h02[0]), mk(l13[0], h13[0]), mk(l02[1], h02[1]), mk(l13[1], h13[1])};
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  conv_terms<0>(mr, X, a);
+  return (a[0] + a[1]) + (a[2] + a[3]);
+}
+__device__ __forceinline__ void load_mrow(const Lds& s, MRow& mr, int lane) {
+#pragma unroll
+  for (int g = 0; g < NF; ++g) mr[g] = s.M[(lane < NF ? lane : 0) * MLD + g];
+}
+#else
+using MRow = double2[MLD / 2];
+__device__ __forceinline__ void load_mrow(const Lds& s, MRow& mr, int lane) {
+#pragma unroll
+  for (int q = 0; q < MLD / 2; ++q) mr[q] = reinterpret_cast<const double2*>(s.M + (lane < NF ? lane : 0) * MLD)[q];
+}
+#endif
+
+#if MH_DPP
+static_assert(MH_RSQ, "the DPP update path takes 1/SIG");
+// One ROI's log-likelihood from the lane's frame operands: t_f and C_R(t_f) (fixed per lane) and Y_{i,f},
+// 1/SIG_{i,f} of ROI i (the sweep reads them one element ahead)
+__device__ __forceinline__ double roi_loglik_r(const Lds& s, const MRow& mreg, int lane, double tv, double cr,
+                                              double y, double rsig, double dvr, double r1, double k2p) {
+  const double k2 = k2p * r1;           // kinetic_model.py:153-154
+  const double k2a = k2 / dvr;
+  const double ex = -k2a * tv;
+  const double ev = lane < NF ? (MH_TEXP ? exp_tab(s.E2, ex) : exp(ex)) : 0.0;   // lanes 54..63: never read
+  const double conv = conv_dpp(mreg, ev);
+  double l = 0.0;
+  if (lane < NF) {
+    const double tac = r1 * cr + (k2 - r1 * k2a) * conv;            // :157-158
+    const double sn = tac < 0.0 ? 1e-6 : tac;                       // mcmc.py:152
+    const double inv = rsq_f64(sn) * rsig;                          // 1 / (sqrt(sn) SIG), :153
+    const double z = (y - sn) * inv;
+    const double xs = sn * inv;
+    const double lnd = xs < 10.0 ? (MH_LOGPHI_POLY ? log_phi_poly(s.LPHI, xs) : log_ndtr(xs)) : 0.0;
+    l = -0.5 * z * z - 0.9189385332046727 + log_pos(inv) - lnd;      // - log sig = log(1 / sig)
+  }
+  __builtin_amdgcn_wave_barrier();
+  return wave_sum(l);
+}
+__device__ __forceinline__ double roi_loglik(const Lds& s, const MRow& mreg, double*, int lane, int i,
+                                            double dvr, double r1, double k2p) {
+  const int fl = lane < NF ? lane : 0;
+  return roi_loglik_r(s, mreg, lane, s.TV[fl], s.CR[fl], s.Y[i * NF + fl], s.SIG[i * NF + fl], dvr, r1, k2p);
+}
+#else
+__device__ __forceinline__ double roi_loglik(const Lds& s, const MRow& mreg, double* e, int lane, int i,
                                             double dvr, double r1, double k2p) {
   const double k2 = k2p * r1;           // kinetic_model.py:153-154
   const double k2a = k2 / dvr;
@@ -255,6 +358,7 @@ __device__ __forceinline__ double roi_loglik(const Lds& s, const double2 (&mreg)
   __builtin_amdgcn_wave_barrier();
   return wave_sum(l);
 }
+#endif
 
 __device__ void load_lds(Lds& s, const MHConst& c) {
   for (int k = threadIdx.x; k < NF * MLD; k += blockDim.x) {
@@ -291,9 +395,8 @@ __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun 
   __shared__ Lds s;
   load_lds(s, c);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  double2 mreg[MLD / 2];
-#pragma unroll
-  for (int q = 0; q < MLD / 2; ++q) mreg[q] = reinterpret_cast<const double2*>(s.M + (lane < NF ? lane : 0) * MLD)[q];
+  MRow mreg;
+  load_mrow(s, mreg, lane);
   double* e = s.E[w];
   double* Zw = s.Z[w];
   double* LUw = s.LU[w];
@@ -302,6 +405,10 @@ __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun 
   const bool own = lane < NR;
   const int li = own ? lane : 0;
   const uint32_t sk0 = (uint32_t)(r.seed & 0xffffffffull), sk1 = (uint32_t)(r.seed >> 32);
+#if MH_DPP && MH_PF
+  const int fl = lane < NF ? lane : 0;
+  const double tvr = s.TV[fl], crr = s.CR[fl];   // the lane's frame time and reference TAC, in registers
+#endif
   for (int chain = blockIdx.x * kWaves + w; chain < r.n_chains; chain += gridDim.x * kWaves) {
     // ---- state: lane l < 48 holds ROI l
     double D = r.x0 ? r.x0[(size_t)chain * 2 * NR + li] : s.MUD[li];
@@ -379,6 +486,10 @@ __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun 
       int k_cur = __builtin_amdgcn_readfirstlane(ORDw[0]);
       int k_nxt = __builtin_amdgcn_readfirstlane(ORDw[1]);
       double z_cur = Zw[k_cur], lu_cur = LUw[k_cur];
+#if MH_DPP
+      const int ic0 = k_cur >= NR ? k_cur - NR : k_cur;   // ROI i's Y and 1/SIG rows, also one element ahead
+      double y_cur = s.Y[ic0 * NF + fl], g_cur = s.SIG[ic0 * NF + fl];
+#endif
 #endif
 #pragma unroll 1
       for (int j = 0; j < 2 * NR; ++j) {
@@ -387,6 +498,10 @@ __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun 
         const int ord2 = ORDw[j + 2 < 2 * NR ? j + 2 : 2 * NR - 1];
         const double z_nxt = Zw[k_nxt], lu_nxt = LUw[k_nxt];
         const double zk = z_cur, luk = lu_cur;
+#if MH_DPP
+        const int inx = k_nxt >= NR ? k_nxt - NR : k_nxt;
+        const double y_nxt = s.Y[inx * NF + fl], g_nxt = s.SIG[inx * NF + fl];
+#endif
 #else
         const int k = __builtin_amdgcn_readfirstlane(ORDw[j]);
 #endif
@@ -406,7 +521,11 @@ __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun 
         const double delta = Zw[k] * si;
 #endif
         const double xp = xi + delta;
+#if MH_DPP && MH_PF
+        const double lln = roi_loglik_r(s, mreg, lane, tvr, crr, y_cur, g_cur, v ? Di : xp, v ? xp : Ri, c.k2p);
+#else
         const double lln = roi_loglik(s, mreg, e, lane, i, v ? Di : xp, v ? xp : Ri, c.k2p);
+#endif
 #if MH_PF
         const double dprior = -0.5 * (2.0 * delta * gi + delta * delta * pii);
 #else
@@ -419,6 +538,10 @@ __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun 
         k_cur = k_nxt;
         z_cur = z_nxt;
         lu_cur = lu_nxt;
+#if MH_DPP
+        y_cur = y_nxt;
+        g_cur = g_nxt;
+#endif
         k_nxt = __builtin_amdgcn_readfirstlane(ord2);
 #else
         const bool acc_ = isfinite(mr) && LUw[k] < mr;
@@ -962,9 +1085,8 @@ __global__ __launch_bounds__(kWaves * 64) void mh_logp_kernel(MHConst c, const d
   __shared__ Lds s;
   load_lds(s, c);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  double2 mreg[MLD / 2];
-#pragma unroll
-  for (int q = 0; q < MLD / 2; ++q) mreg[q] = reinterpret_cast<const double2*>(s.M + (lane < NF ? lane : 0) * MLD)[q];
+  MRow mreg;
+  load_mrow(s, mreg, lane);
   double* e = s.E[w];
   const int li = lane < NR ? lane : 0;
   for (int pt = blockIdx.x * kWaves + w; pt < n; pt += gridDim.x * kWaves) {
