@@ -101,6 +101,39 @@ __device__ __forceinline__ void load_e2(double* E2) {
   for (int j = threadIdx.x; j < kE2; j += blockDim.x) E2[j] = exp2((double)j / kE2);
 }
 
+// Round 6: log x (x > 0 finite) from a 64-entry table over the mantissa: m = x 2^-e in [1, 2), row j = floor(64 (m - 1))
+// holds (1/c_j rounded, -log of that), c_j = 1 + (j + 1/2) / 64; r = m / c_j - 1 by one fma (|r| <= 1/128), log(1 + r)
+// by its degree-8 Taylor polynomial (truncation 5e-20).  Absolute error < 1 ulp of max(|log x|, 1) (numpy check in
+// DESIGN.md §3), the measure that matters in a sum of 54 frame terms.  Replaces fdlibm's division f / (2 + f) and its
+// 14 polynomial / combination steps.  Otherwise (0, negative, inf, NaN, denormal): ocml's log.  0: log_pos
+#ifndef MH_TLOG
+#define MH_TLOG 1
+#endif
+constexpr int kLT = 64;
+__device__ __forceinline__ double log_tab(const double2* LT, double x) {
+  if (!(x >= 2.2250738585072014e-308 && x < __builtin_huge_val())) return log(x);
+  const int e = __builtin_amdgcn_frexp_exp(x) - 1;                     // x = m 2^e, m in [1, 2)
+  const double m = __builtin_amdgcn_frexp_mant(x) * 2.0;
+  const int j = (int)((m - 1.0) * 64.0);                               // exact: m - 1 and the scaling
+  const double2 t = LT[j];                                             // (1/c, -log(1/c))
+  const double r = fma(m, t.x, -1.0);
+  double p = -0.125;                                                   // -1/8
+  p = fma(p, r, 1.4285714285714285e-01);
+  p = fma(p, r, -1.6666666666666666e-01);
+  p = fma(p, r, 0.2);
+  p = fma(p, r, -0.25);
+  p = fma(p, r, 3.3333333333333333e-01);
+  p = fma(p, r, -0.5);
+  const double l1p = fma(p * r, r, r);                                 // r - r^2/2 + ... - r^8/8
+  return fma((double)e, 6.93147180369123816490e-01, fma((double)e, 1.90821492927058770002e-10, t.y + l1p));
+}
+__device__ __forceinline__ void load_lt(double2* LT) {
+  for (int j = threadIdx.x; j < kLT; j += blockDim.x) {
+    const double inv = 1.0 / (1.0 + (j + 0.5) / kLT);
+    LT[j] = make_double2(inv, -log(inv));
+  }
+}
+
 // e^{-k2a t} of the update kernel by fp64_math.h exp_fast (<= 1 ulp) instead of ocml's exp
 #ifndef MH_FAST_EXP
 #define MH_FAST_EXP 0
@@ -151,6 +184,7 @@ struct Lds {
   double MUD[NR], MUR[NR];
   alignas(16) double LPHI[LPNI * LPLD];   // log Phi polynomial (16-B aligned rows)
   double E2[kE2];                         // 2^(j/64) (MH_TEXP)
+  double2 LT[kLT];                        // (1/c_j, -log(1/c_j)) (MH_TLOG)
   double E[kWaves][64];               // per-wave exponential scratch
   double Z[kWaves][2 * NR];           // per-wave sweep draws: N(0,1) proposal per element
   double LU[kWaves][2 * NR];          //   log accept-uniform per element
@@ -287,7 +321,7 @@ __device__ __forceinline__ double roi_loglik_r(const Lds& s, const MRow& mreg, i
     const double z = (y - sn) * inv;
     const double xs = sn * inv;
     const double lnd = xs < 10.0 ? (MH_LOGPHI_POLY ? log_phi_poly(s.LPHI, xs) : log_ndtr(xs)) : 0.0;
-    l = -0.5 * z * z - 0.9189385332046727 + log_pos(inv) - lnd;      // - log sig = log(1 / sig)
+    l = -0.5 * z * z - 0.9189385332046727 + (MH_TLOG ? log_tab(s.LT, inv) : log_pos(inv)) - lnd;   // - log sig
   }
   __builtin_amdgcn_wave_barrier();
   return wave_sum(l);
@@ -371,6 +405,7 @@ __device__ void load_lds(Lds& s, const MHConst& c) {
   for (int k = threadIdx.x; k < NR; k += blockDim.x) { s.MUD[k] = c.MUD[k]; s.MUR[k] = c.MUR[k]; }
   load_logphi(s.LPHI);
   load_e2(s.E2);
+  load_lt(s.LT);
   __syncthreads();
 }
 
