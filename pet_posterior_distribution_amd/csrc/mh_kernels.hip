@@ -694,6 +694,7 @@ struct LdsB {
   double MUD[NR], MUR[NR];
   alignas(16) double LPHI[LPNI * LPLD];   // log Phi polynomial (16-B aligned rows)
   double E2[kE2];                         // 2^(j/64) (MH_TEXP)
+  double2 LT[kLT];                        // (1/c_j, -log(1/c_j)) (MH_TLOG)
   double W[kBW][kWD];                 // per wave: e rows [q][MLD] / frame terms [q][64] / sweep draws
   double P[kBW][kQ * 4];              // per wave: the batch's (R1, k2, k2a, roi)
   double LL[kBW][kNE];                // per chain group: the draw's evaluations
@@ -778,7 +779,7 @@ __device__ __forceinline__ void eval_batch(const LdsB& s, double* W, double* P, 
       const double lnd = xs < 10.0 ? (MH_LOGPHI_POLY ? log_phi_poly(s.LPHI, xs)
                                                       : log(0.5 * erfc(-xs * 0.7071067811865476))) : 0.0;
 #if MH_RSQ
-      l = -0.5 * z * z - 0.9189385332046727 + log_pos(inv) - lnd;
+      l = -0.5 * z * z - 0.9189385332046727 + (MH_TLOG ? log_tab(s.LT, inv) : log_pos(inv)) - lnd;
 #else
       l = -0.5 * z * z - 0.9189385332046727 - (MH_FAST_LOG ? log_pos(sig) : log(sig)) - lnd;
 #endif
@@ -816,6 +817,7 @@ __global__ __launch_bounds__(kBW * 64) void mh_chain_batched(MHConst c, MHRun r)
   for (int k = threadIdx.x; k < NR; k += blockDim.x) { s.MUD[k] = c.MUD[k]; s.MUR[k] = c.MUR[k]; }
   load_logphi(s.LPHI);
   load_e2(s.E2);
+  load_lt(s.LT);
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int grp = w / WPC, rk = w - grp * WPC;
