@@ -86,3 +86,35 @@ def test_level_outputs_invalid_after_generate():
     with pytest.raises(Exception, match='B exceeds'):
         m.level_outputs(B=8)
     m.close()
+
+
+def test_rccl_stats_gather_world1():
+    """The configs[3] collective over RCCL on the box's GPU: a one-rank 'nccl' group (the only RCCL group a
+    1-GPU box can form; RCCL refuses two ranks on one device), device-side fp64 all-gather of a rank's
+    per-TAC Welford partials through gather_merge_own_tacs, then the host merge.  World 1 makes the result
+    the rank's own partials, so it must come back bitwise; the N > 1 merge itself is the gloo test's
+    (tests/test_cpu_sharded.py)."""
+    import os
+    import socket
+    import torch.distributed as dist
+    from pet_posterior_distribution_amd.distributed import gather_merge_own_tacs
+    assert not dist.is_initialized()
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    os.environ.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    dist.init_process_group('nccl', init_method=f'tcp://127.0.0.1:{port}', rank=0, world_size=1,
+                            device_id=torch.device('cuda', 0))
+    try:
+        assert dist.get_backend() == 'nccl'
+        rng = np.random.default_rng(5)
+        n_tac, n_per = 6, 10
+        local = np.zeros((n_tac, 48, 2, 3))
+        local[..., 0] = n_per
+        local[..., 1] = rng.standard_normal((n_tac, 48, 2))
+        local[..., 2] = rng.uniform(0.5, 2.0, (n_tac, 48, 2))
+        got = gather_merge_own_tacs(local, n_tac, n_per, device=torch.device('cuda', 0))
+        np.testing.assert_array_equal(got, local)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
