@@ -83,8 +83,17 @@ __device__ __forceinline__ double rsq_f64(double x) {
 #define MH_TEXP 1
 #endif
 constexpr int kE2 = 64;
+#ifndef MH_BRANCHLESS
+#define MH_BRANCHLESS 1
+#endif
 __device__ __forceinline__ double exp_tab(const double* E2, double x) {
+#if MH_BRANCHLESS
+  // x clamped to [-746, 710] instead of a branch to ocml: below, e^x rounds to 0 (ldexp), above it overflows
+  // to inf; NaN passes the clamp and the reduction as NaN; (-745, -708) gives denormals by ldexp
+  x = x < -746.0 ? -746.0 : (x > 710.0 ? 710.0 : x);
+#else
   if (!(x > -708.0 && x < 709.0)) return exp(x);
+#endif
   const double kf = rint(x * 92.332482616893656);                 // 64 / ln 2
   double r = fma(-kf, 6.93147180369123816490e-01 / 64, x);       // fdlibm's ln 2 split (kf ln2_hi exact), / 64
   r = fma(-kf, 1.90821492927058770002e-10 / 64, r);
@@ -111,10 +120,16 @@ __device__ __forceinline__ void load_e2(double* E2) {
 #endif
 constexpr int kLT = 64;
 __device__ __forceinline__ double log_tab(const double2* LT, double x) {
+#if !MH_BRANCHLESS
   if (!(x >= 2.2250738585072014e-308 && x < __builtin_huge_val())) return log(x);
+#endif
   const int e = __builtin_amdgcn_frexp_exp(x) - 1;                     // x = m 2^e, m in [1, 2)
   const double m = __builtin_amdgcn_frexp_mant(x) * 2.0;
+#if MH_BRANCHLESS
+  const int j = min(max((int)((m - 1.0) * 64.0), 0), 63);            // rows 0..63 for 0 / inf / NaN too
+#else
   const int j = (int)((m - 1.0) * 64.0);                               // exact: m - 1 and the scaling
+#endif
   const double2 t = LT[j];                                             // (1/c, -log(1/c))
   const double r = fma(m, t.x, -1.0);
   double p = -0.125;                                                   // -1/8
@@ -125,7 +140,13 @@ __device__ __forceinline__ double log_tab(const double2* LT, double x) {
   p = fma(p, r, 3.3333333333333333e-01);
   p = fma(p, r, -0.5);
   const double l1p = fma(p * r, r, r);                                 // r - r^2/2 + ... - r^8/8
-  return fma((double)e, 6.93147180369123816490e-01, fma((double)e, 1.90821492927058770002e-10, t.y + l1p));
+  const double res = fma((double)e, 6.93147180369123816490e-01, fma((double)e, 1.90821492927058770002e-10, t.y + l1p));
+#if MH_BRANCHLESS
+  // denormals take the table path (frexp normalises them); 0 -> -inf, < 0 -> NaN, inf -> inf, NaN -> NaN
+  return x > 0.0 ? (x < __builtin_huge_val() ? res : x) : (x == 0.0 ? -__builtin_huge_val() : __builtin_nan(""));
+#else
+  return res;
+#endif
 }
 __device__ __forceinline__ void load_lt(double2* LT) {
   for (int j = threadIdx.x; j < kLT; j += blockDim.x) {
