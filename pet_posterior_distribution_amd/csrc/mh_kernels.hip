@@ -86,6 +86,9 @@ constexpr int kE2 = 64;
 #ifndef MH_BRANCHLESS
 #define MH_BRANCHLESS 1
 #endif
+#ifndef MH_FRAME_SELECT
+#define MH_FRAME_SELECT 1     // the update's frame terms on every lane, masked by a select (roi_loglik_r)
+#endif
 __device__ __forceinline__ double exp_tab(const double* E2, double x) {
 #if MH_BRANCHLESS
   // x clamped to [-746, 710] instead of a branch to ocml: below, e^x rounds to 0 (ldexp), above it overflows
@@ -332,6 +335,21 @@ __device__ __forceinline__ double roi_loglik_r(const Lds& s, const MRow& mreg, i
   const double k2 = k2p * r1;           // kinetic_model.py:153-154
   const double k2a = k2 / dvr;
   const double ex = -k2a * tv;
+#if MH_FRAME_SELECT && MH_BRANCHLESS && MH_TEXP && MH_TLOG && MH_LOGPHI_POLY
+  // every lane runs the frame terms (lanes 54..63 on frame 0's operands) and the frame mask is a select at
+  // the end: no exec-mask branches on the update's critical path
+  const double ev = exp_tab(s.E2, ex);                            // lanes 54..63: never read by conv_dpp
+  const double conv = conv_dpp(mreg, ev);
+  const double tac = r1 * cr + (k2 - r1 * k2a) * conv;            // :157-158
+  const double sn = tac < 0.0 ? 1e-6 : tac;                       // mcmc.py:152
+  const double inv = rsq_f64(sn) * rsig;                          // 1 / (sqrt(sn) SIG), :153
+  const double z = (y - sn) * inv;
+  const double xs = sn * inv;
+  const double lp = log_phi_poly(s.LPHI, xs);                     // row clamped to [0, 9] for any xs
+  const double lnd = xs < 10.0 ? lp : 0.0;
+  const double lf = -0.5 * z * z - 0.9189385332046727 + log_tab(s.LT, inv) - lnd;   // - log sig
+  const double l = lane < NF ? lf : 0.0;
+#else
   const double ev = lane < NF ? (MH_TEXP ? exp_tab(s.E2, ex) : exp(ex)) : 0.0;   // lanes 54..63: never read
   const double conv = conv_dpp(mreg, ev);
   double l = 0.0;
@@ -344,6 +362,7 @@ __device__ __forceinline__ double roi_loglik_r(const Lds& s, const MRow& mreg, i
     const double lnd = xs < 10.0 ? (MH_LOGPHI_POLY ? log_phi_poly(s.LPHI, xs) : log_ndtr(xs)) : 0.0;
     l = -0.5 * z * z - 0.9189385332046727 + (MH_TLOG ? log_tab(s.LT, inv) : log_pos(inv)) - lnd;   // - log sig
   }
+#endif
   __builtin_amdgcn_wave_barrier();
   return wave_sum(l);
 }
