@@ -839,62 +839,89 @@ __device__ __forceinline__ void store_act(T* base, size_t row, int C, int n, con
   else Vec8<T>::store(base + row * C + n, v);
 }
 
+// One down0 position pair (pooled position lp of sample b0 + bl, pos = 24 bl + lp): x from LDS (xs [nb][96]),
+// maps from LDS (mp [48][128], FAST) or global, weights in registers; 8 channels n0 .. n0 + 7.
+template <typename T, int XS, bool FAST>
+__device__ __forceinline__ void down0_pos(const Down0Args& a, const float* xs, const float* mp, int b0,
+                                          const f32x4 (&wr)[12][2], int n0, int pos) {
+  const int bl = pos / 24, lp = pos - bl * 24, b = b0 + bl;
+  const int l0 = 2 * lp;
+  float xv[7][2];
+#pragma unroll
+  for (int q = 0; q < 7; ++q) {
+    const int p = l0 - 2 + q;
+    const bool ok = (p >= 0 && p < 48);
+    xv[q][0] = ok ? xs[bl * 96 + p * 2] : 0.f;
+    xv[q][1] = ok ? xs[bl * 96 + p * 2 + 1] : 0.f;
+  }
+  float v[2][8];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int l = l0 + e;
+    f32x4 m0, m1;
+    if constexpr (FAST) {
+      m0 = *reinterpret_cast<const f32x4*>(mp + l * 128 + n0);
+      m1 = *reinterpret_cast<const f32x4*>(mp + l * 128 + n0 + 4);
+    } else {
+      const int tac = a.tac ? a.tac[b] : 0;
+      const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[b];
+      const float* tmr = a.tmap + ((size_t)t * 48 + l) * 128 + n0;
+      const float* cmr = a.cmap + ((size_t)tac * 48 + l) * 128 + n0;
+      m0 = *reinterpret_cast<const f32x4*>(tmr) + *reinterpret_cast<const f32x4*>(cmr);
+      m1 = *reinterpret_cast<const f32x4*>(tmr + 4) + *reinterpret_cast<const f32x4*>(cmr + 4);
+    }
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        acc0 += wr[j * 2 + c][0] * xv[e + j][c];
+        acc1 += wr[j * 2 + c][1] * xv[e + j][c];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[e][q] = fmaxf(acc0[q] + m0[q], 0.f);
+      v[e][4 + q] = fmaxf(acc1[q] + m1[q], 0.f);
+    }
+    if constexpr (!(FIN_EXP & 2)) store_act<T, XS>(reinterpret_cast<T*>(a.s0), (size_t)b * 48 + l, 128, n0, v[e]);
+    else if (v[e][0] == 12345.f) reinterpret_cast<T*>(a.s0)[0] = (T)0.f;
+  }
+  float pv[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) pv[q] = fmaxf(v[0][q], v[1][q]);
+  if constexpr (!(FIN_EXP & 2)) store_act<T, XS>(reinterpret_cast<T*>(a.p0), (size_t)b * 24 + lp, 128, n0, pv);
+  else if (pv[0] == 12345.f) reinterpret_cast<T*>(a.p0)[0] = (T)0.f;
+}
+
+// Round 6: CONV_D0_PAIR positions in flight per thread (independent position pairs in one basic block, so
+// their LDS reads, FMA chains and stores interleave; the epilogue runs one wave per SIMD, so nothing else
+// hides a lone position's latency).  1: one at a time.
+#ifndef CONV_D0_PAIR
+#define CONV_D0_PAIR 3
+#endif
+template <typename T, int XS, bool FAST>
+__device__ __forceinline__ void down0_loop(const Down0Args& a, const float* xs, const float* mp, int b0, int nb,
+                                           const f32x4 (&wr)[12][2], int n0, int pos0, int pstride) {
+  const int n = nb * 24;
+  if (CONV_D0_PAIR > 1 && n % (CONV_D0_PAIR * pstride) == 0) {
+    for (int pos = pos0; pos < n; pos += CONV_D0_PAIR * pstride) {
+#pragma unroll
+      for (int u = 0; u < CONV_D0_PAIR; ++u) down0_pos<T, XS, FAST>(a, xs, mp, b0, wr, n0, pos + u * pstride);
+    }
+  } else {
+    for (int pos = pos0; pos < n; pos += pstride) down0_pos<T, XS, FAST>(a, xs, mp, b0, wr, n0, pos);
+  }
+}
+
 // down0 positions pos0, pos0 + pstride, ... of samples b0 .. b0 + nb - 1: x from LDS
 // (xs [nb][96]), maps from LDS (mp [48][128], fast) or global, weights in registers.
 template <typename T, int XS = 0>
 __device__ __forceinline__ void down0_positions(const Down0Args& a, const float* xs, const float* mp, bool fast,
                                                 int b0, int nb, const f32x4 (&wr)[12][2], int n0, int pos0,
                                                 int pstride) {
-  for (int pos = pos0; pos < nb * 24; pos += pstride) {
-    const int bl = pos / 24, lp = pos - bl * 24, b = b0 + bl;
-    const int l0 = 2 * lp;
-    float xv[7][2];
-#pragma unroll
-    for (int q = 0; q < 7; ++q) {
-      const int p = l0 - 2 + q;
-      const bool ok = (p >= 0 && p < 48);
-      xv[q][0] = ok ? xs[bl * 96 + p * 2] : 0.f;
-      xv[q][1] = ok ? xs[bl * 96 + p * 2 + 1] : 0.f;
-    }
-    float v[2][8];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int l = l0 + e;
-      f32x4 m0, m1;
-      if (fast) {
-        m0 = *reinterpret_cast<const f32x4*>(mp + l * 128 + n0);
-        m1 = *reinterpret_cast<const f32x4*>(mp + l * 128 + n0 + 4);
-      } else {
-        const int tac = a.tac ? a.tac[b] : 0;
-        const int t = a.t_uniform >= 0 ? a.t_uniform : a.tvec[b];
-        const float* tmr = a.tmap + ((size_t)t * 48 + l) * 128 + n0;
-        const float* cmr = a.cmap + ((size_t)tac * 48 + l) * 128 + n0;
-        m0 = *reinterpret_cast<const f32x4*>(tmr) + *reinterpret_cast<const f32x4*>(cmr);
-        m1 = *reinterpret_cast<const f32x4*>(tmr + 4) + *reinterpret_cast<const f32x4*>(cmr + 4);
-      }
-      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          acc0 += wr[j * 2 + c][0] * xv[e + j][c];
-          acc1 += wr[j * 2 + c][1] * xv[e + j][c];
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        v[e][q] = fmaxf(acc0[q] + m0[q], 0.f);
-        v[e][4 + q] = fmaxf(acc1[q] + m1[q], 0.f);
-      }
-      if constexpr (!(FIN_EXP & 2)) store_act<T, XS>(reinterpret_cast<T*>(a.s0), (size_t)b * 48 + l, 128, n0, v[e]);
-      else if (v[e][0] == 12345.f) reinterpret_cast<T*>(a.s0)[0] = (T)0.f;
-    }
-    float pv[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) pv[q] = fmaxf(v[0][q], v[1][q]);
-    if constexpr (!(FIN_EXP & 2)) store_act<T, XS>(reinterpret_cast<T*>(a.p0), (size_t)b * 24 + lp, 128, n0, pv);
-    else if (pv[0] == 12345.f) reinterpret_cast<T*>(a.p0)[0] = (T)0.f;
-  }
+  if (fast) down0_loop<T, XS, true>(a, xs, mp, b0, nb, wr, n0, pos0, pstride);
+  else down0_loop<T, XS, false>(a, xs, mp, b0, nb, wr, n0, pos0, pstride);
 }
 
 // Round 6: down0 on the MFMA array for the 16-bit networks (CONV_DOWN0_MFMA).  For a group of 4 samples and the
