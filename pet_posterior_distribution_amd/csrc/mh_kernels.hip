@@ -86,6 +86,9 @@ constexpr int kE2 = 64;
 #ifndef MH_BRANCHLESS
 #define MH_BRANCHLESS 1
 #endif
+#ifndef MH_SEL_BCAST
+#define MH_SEL_BCAST 1
+#endif
 #ifndef MH_FRAME_SELECT
 #define MH_FRAME_SELECT 1     // the update's frame terms on every lane, masked by a select (roi_loglik_r)
 #endif
@@ -587,8 +590,15 @@ __global__ __launch_bounds__(kWaves * 64) void mh_chain_kernel(MHConst c, MHRun 
 #endif
         const double Di = lane_bcast(D, i), Ri = lane_bcast(R, i);
         const double xi = v ? Ri : Di;
+#if MH_SEL_BCAST
+        // the element's scale and prior gradient: per-lane select on the (uniform) v, then one broadcast each
+        // (no branch between two readlane pairs)
+        const double si = lane_bcast(v ? sR : sD, i);
+        const double gi = lane_bcast(v ? gR : gD, i);
+#else
         const double si = v ? lane_bcast(sR, i) : lane_bcast(sD, i);
         const double gi = v ? lane_bcast(gR, i) : lane_bcast(gD, i);
+#endif
         const double lli = lane_bcast(ll, i);
 #if MH_PF
         const double delta = zk * si;
